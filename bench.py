@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident masked CRC32C over 4 KiB blocks.
+
+BASELINE.json metric "GiB/s CRC32C over 4 KiB blocks (device-resident); % of HBM
+read roofline", workload = config C2 (1M x 4 KiB random blocks per GPU, bit-exact
+vs the reference algorithm).  One step = one pass of the engine over the whole
+1M-block batch (jl_crc32c_fixed_dev), inputs resident in HBM.  With N GPUs
+(torchrun, one process per GPU) every rank holds its own 1M-block shard of the
+C4 8M-block set, generated in place (weak scaling, no data-path collective);
+value = all ranks' bytes / max-over-ranks time.
+
+Also reported on the same JSON line:
+  roofline     — dominant kernel (crc_fixed4k_kernel) timed with HIP events on
+                 its launch stream; algorithmic bytes = 4096 B read + 4 B
+                 written per block; peak = 8.0 TB/s (MI355X spec);
+                 measured read-stream ceiling beside it; traffic from the
+                 committed rocprofv3 PMC summary (profiles/) when present.
+  cpu_baseline — rank 0 at N=1: the CPU oracle (restatement of the reference's
+                 slicing-by-8 Crc32C.update) on a 1 GiB sample of the same
+                 blocks, looped for ~10 s; parity of that sample checked.
+  secondary    — configs C3 (mixed Zipf sizes) and C5 (WAL verify), N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import jleveldb_amd as jl  # noqa: E402
+
+SEED = 0x4A4C4442
+PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+GIB = float(1 << 30)
+
+
+def timed(fn, steps, warmup, stream):
+    """Runs fn() warmup+steps times; returns (wall_s, event_ms) of the timed steps."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, e0.elapsed_time(e1)
+
+
+def read_stream_ceiling(data, stream) -> float:
+    sink = torch.zeros(1, dtype=torch.int32, device=data.device)
+    _, ms = timed(lambda: jl.read_stream_dev(data, sink), 10, 3, stream)
+    return data.numel() / (ms / 10 / 1e3) / 1e9
+
+
+def pmc_traffic():
+    """HBM bytes per launch of crc_fixed4k_kernel from the committed PMC summary."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*fixed4k*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
+def cpu_baseline(data, n_blocks, gpu_out, seconds):
+    from oracle import oracle  # cpu_baseline leg only (test infrastructure)
+
+    sample_blocks = min(n_blocks, 1 << 18)  # 1 GiB
+    host = data[: sample_blocks * 4096].cpu().numpy()
+    threads = min(16, os.cpu_count() or 1)
+    want = oracle.fixed(host, 4096, sample_blocks, threads=threads)
+    parity = bool(np.array_equal(want, gpu_out[:sample_blocks]))
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        oracle.fixed(host, 4096, sample_blocks, threads=threads)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    t1 = time.perf_counter()
+    oracle.fixed(host[: 1 << 26], 4096, 1 << 14, threads=1)
+    one = (1 << 26) / (time.perf_counter() - t1) / GIB
+    return {
+        "value": round(done * sample_blocks * 4096 / el / GIB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample_blocks} x 4 KiB blocks (1 GiB) of the same data, {done} passes in {el:.1f} s; "
+                  f"oracle/crc32c_oracle.c slicing-by-8 restatement of Crc32C.update; 1-thread rate {one:.2f} GiB/s",
+        "parity_with_gpu": parity,
+    }
+
+
+def secondary_c3(dev, stream, steps, warmup):
+    """Config C3: 1M blocks, k~Zipf(1.1) on 1..64, len = 1024(k-1)+1+U[0,1023], packed, unaligned."""
+    rng = np.random.default_rng(SEED)
+    n = 1 << 20
+    ks = np.empty(0, dtype=np.int64)
+    while ks.size < n:
+        k = rng.zipf(1.1, 2 * n)
+        ks = np.concatenate([ks, k[k <= 64]])
+    ks = ks[:n]
+    lens = (1024 * (ks - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    arena = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    jl.fill_random_dev(arena, SEED + 3)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    wall, ms = timed(lambda: jl.crc32c_batch_dev(arena, d_off, d_len, out=out), steps, warmup, stream)
+    alg = total + n * (4 + 12)
+    res = {"config": "C3 1M mixed Zipf 1 B-64 KiB blocks, one arena, unaligned", "bytes": total,
+           "GiB_per_s": round(total / (ms / steps / 1e3) / GIB, 1),
+           "achieved_GBps": round(alg / (ms / steps / 1e3) / 1e9, 1), "ms_per_step": round(ms / steps, 3)}
+    del arena
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blocks", type=int, default=1 << 20, help="4 KiB blocks per GPU (C2: 1M)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    jl.init(local)
+    stream = torch.cuda.current_stream()
+
+    n = args.blocks
+    data = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
+    # rank r holds blocks [r*n, (r+1)*n) of the C4 set, generated in place
+    jl.fill_random_dev(data, SEED, first_word=rank * n * 512)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    step = lambda: jl.crc32c_fixed_dev(data, 4096, n, out=out)  # noqa: E731
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / args.steps
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+
+    bytes_step = world * n * 4096
+    value = bytes_step * args.steps / wall / GIB
+    alg_launch = n * (4096 + 4)
+    achieved = alg_launch / (kern_ms / 1e3) / 1e9
+    result = None
+    if rank == 0:
+        gpu_out = out.cpu().numpy().view(np.uint32)
+        traffic, traffic_src = pmc_traffic()
+        ceiling = read_stream_ceiling(data, stream)
+        result = {
+            "metric": "GiB/s CRC32C over 4 KiB blocks (device-resident); % of HBM read roofline",
+            "value": round(value, 1),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device splitmix64, seed 0x4A4C4442; rank r = blocks [r*1M,(r+1)*1M) of the C4 set)",
+            "config": {"workload": "C2: 1M x 4 KiB random blocks per GPU, masked CRC32C, device-resident",
+                       "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "crc_fixed4k_kernel",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_GBS, 4),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel_ms": round(kern_ms, 4),
+                "alg_bytes_per_launch": alg_launch,
+                "read_stream_ceiling_GBps": round(ceiling, 1),
+                "frac_of_read_ceiling": round(achieved / ceiling, 4),
+            },
+        }
+        if world == 1 and not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(data, n, gpu_out, args.cpu_seconds)
+    if world == 1 and not args.no_secondary:
+        del data
+        torch.cuda.empty_cache()
+        result["secondary"] = [secondary_c3(dev, stream, 5, 2)]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+/*
+ * jlcrc.h — C-ABI of the MI355X-native masked-CRC32C engine for jleveldb.
+ *
+ * Drop-in boundary for the reference's checksum path.  J below abbreviates
+ * src/main/java/com/tchaicatkovsky/jleveldb in ralgond/jleveldb.  The reference
+ * has no FFI of its own: every entry point names the Java member it replaces;
+ * INTEGRATION.md shows the JNI binding a maintainer adds on the Java side.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; every function is callable from C and JNI;
+ *   - int-returning functions return JL_OK (0) or a negative JL_ERR_* code and
+ *     never throw; jl_last_error() gives a thread-local message;
+ *   - "_dev" functions take device pointers (HBM) and an optional hipStream_t
+ *     (void*; NULL = the engine's own stream) and are asynchronous unless noted;
+ *     the other batch functions take host memory and block until done;
+ *   - there is no CPU fallback behind the batch / verify entry points: with no
+ *     usable GPU they fail with JL_ERR_NO_DEVICE.  Only the scalar Crc32C
+ *     statics (first block) run on the host, as the reference's do.
+ */
+#ifndef JLCRC_H
+#define JLCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+#define JL_OK 0
+#define JL_ERR_INVALID (-1)   /* bad argument (null pointer, size overflow)      */
+#define JL_ERR_NO_DEVICE (-2) /* no HIP device / engine built without a GPU     */
+#define JL_ERR_HIP (-3)       /* HIP runtime error (message in jl_last_error)   */
+#define JL_ERR_NOMEM (-4)     /* device or pinned-host allocation failed         */
+#define JL_ERR_CAPACITY (-5)  /* caller's output array too small                 */
+
+/* flags for the batch entry points */
+#define JL_FLAG_MASK 1u /* store Crc32C.mask(crc) (the on-disk form), else the raw crc */
+
+/* -------------------------------------------------- Crc32C statics (host) */
+/* Replaces Crc32C.value(byte[],int,int) / value(Slice), J/util/Crc32C.java:85-93 */
+uint32_t jl_crc32c_value(const uint8_t *data, size_t n);
+/* Replaces Crc32C.extend(long,byte[],int,int), J/util/Crc32C.java:43-48 */
+uint32_t jl_crc32c_extend(uint32_t init_crc, const uint8_t *data, size_t n);
+/* Replaces Crc32C.mask(long), J/util/Crc32C.java:61-64 */
+uint32_t jl_crc32c_mask(uint32_t crc);
+/* Replaces Crc32C.unmask(long), J/util/Crc32C.java:72-75 */
+uint32_t jl_crc32c_unmask(uint32_t masked_crc);
+/* Replaces the java.util.zip.Checksum instance state of Crc32C
+ * (J/util/Crc32C.java:96-167): `state` is the bit-flipped crc the Java object
+ * holds in its `crc` field.  reset() == 0xffffffff; getValue() == ~state;
+ * setValue(v) == ~v.  update(int b) is jl_crc32c_update(state, &b, 1). */
+uint32_t jl_crc32c_update(uint32_t state, const uint8_t *data, size_t n);
+
+/* --------------------------------------------------------------- lifecycle */
+/* Binds the calling process to HIP device `device` (0-based ordinal within
+ * HIP_VISIBLE_DEVICES), uploads the LDS table image and creates the engine
+ * stream.  Idempotent for the same device.  (No reference counterpart: the Java
+ * class is static; the JNI adapter calls this from its static initialiser.) */
+int jl_init(int device);
+int jl_shutdown(void);
+const char *jl_last_error(void);
+/* Number of visible HIP devices (0 when none). */
+int jl_device_count(void);
+/* Engine build/version string, e.g. "jlcrc 0.1 gfx950". */
+const char *jl_version(void);
+
+/* ------------------------------------------ device-resident batch checksums */
+/* n_blocks contiguous blocks of block_bytes each starting at d_data
+ * (block i = d_data[i*block_bytes, (i+1)*block_bytes)); d_out[i] = crc32c of
+ * block i (masked with JL_FLAG_MASK).  The DBBench "crc32c" shape
+ * (J/benchmark/DBBench.java:775-793) batched; block_bytes may be any size. */
+int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags,
+                        uint32_t *d_out, void *stream);
+
+/* Arbitrary blocks in one arena: block i = d_base[d_off[i], d_off[i]+d_len[i]).
+ * d_init (nullable): per-block initial crc as in Crc32C.extend(init, ...),
+ *   J/util/Crc32C.java:43-48 (LogWriter uses typeCrc[t], J/db/LogWriter.java:147).
+ * d_suffix (nullable): one extra byte appended after each block, as
+ *   TableBuilder.writeRawBlock appends the type byte, J/table/TableBuilder.java:313-315.
+ * d_out[i] = crc (or mask(crc) with JL_FLAG_MASK). */
+int jl_crc32c_batch_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint32_t *d_init,
+                        const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out, void *stream);
+
+/* Host-memory form of jl_crc32c_batch_dev: stages base[0, base_bytes) and the
+ * descriptors through pinned buffers to the device, runs the kernel, copies the
+ * results back and returns when out[] is filled. */
+int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *off, const uint32_t *len,
+                    const uint32_t *init, const uint8_t *suffix, uint64_t n, uint32_t flags, uint32_t *out);
+
+/* ----------------------------------------------------- SSTable block shims */
+/* Write side, batched TableBuilder.writeRawBlock (J/table/TableBuilder.java:305-323):
+ * for block i = d_file[d_off[i], d_off[i]+d_size[i]) with compression type
+ * d_type[i] (nullable = 0, kNoCompression, J/CompressionType.java) writes the
+ * 5-byte trailer [type][LE32 mask(crc32c(block || type))] to d_trailer[5*i]. */
+int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, const uint8_t *d_type,
+                          uint64_t n, uint8_t *d_trailer, void *stream);
+
+/* Read side, batched TableFormat.readBlock checksum test
+ * (J/table/TableFormat.java:207-218): for handle i (offset d_off[i], size
+ * d_size[i]; the block plus its trailer must lie inside the file) sets
+ * d_status[i] = 1 when unmask(LE32 @ off+size+1) == crc32c(file[off, off+size+1)),
+ * else 0 ("block checksum mismatch"). */
+int jl_table_verify_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, uint64_t n,
+                        uint8_t *d_status, void *stream);
+/* Host-memory form (file = mmap'd .ldb bytes); blocking. */
+int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *off, const uint32_t *size, uint64_t n,
+                    uint8_t *status);
+
+/* ------------------------------------------------- WAL / MANIFEST log shims */
+/* One physical-record decision of LogReader.readPhysicalRecord
+ * (J/db/LogReader.java:297-383), in file order. */
+typedef struct jl_log_event {
+    uint64_t offset; /* file offset of the 7-byte header                     */
+    uint32_t length; /* header length field                                   */
+    uint8_t type;    /* header type byte (J/db/LogFormat.java:28-48)           */
+    uint8_t kind;    /* JL_LOG_* below                                        */
+    uint16_t pad;
+} jl_log_event;
+
+#define JL_LOG_OK 1             /* record accepted (CRC verified when checksum=1)             */
+#define JL_LOG_BAD_CRC 2        /* "checksum mismatch": rest of the 32 KiB block dropped :356-369 */
+#define JL_LOG_BAD_LENGTH 3     /* "bad record length": rest of block dropped :334-345        */
+#define JL_LOG_ZERO_SKIP 4      /* type 0, length 0: rest of block skipped silently :347-353  */
+#define JL_LOG_EOF_BAD_LENGTH 5 /* length past end of the final, short block: EOF :341-344    */
+#define JL_LOG_EOF_TRUNC 6      /* 1..6 stray bytes at the end of the final block: EOF :315-322 */
+
+/* Device-resident log verification: walks every 32 KiB block's headers,
+ * verifies every record's masked CRC (crc over type || payload, LogWriter.java:147)
+ * and truncates each block after its first failure, exactly as the reference
+ * reader clears its buffer.  Writes up to `cap` events to d_events and the total
+ * to *n_events (host pointer; this call synchronises on the stream). */
+int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
+                      uint64_t *n_events, void *stream);
+/* Host-memory form (log = the on-disk .log / MANIFEST bytes); blocking. */
+int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_event *events, uint64_t cap,
+                  uint64_t *n_events);
+
+/* LogReader.readRecord over a whole file (J/db/LogReader.java:146-252), driven
+ * by jl_log_verify's events: reassembles fragmented records and produces the
+ * same corruption reports the reference Reporter receives.
+ *   records[i] = {offset (lastRecordOffset), arena offset, size}; payloads are
+ *   appended to `arena`; reports[i] = {dropped bytes, reason, aux (type for
+ *   JL_REASON_UNKNOWN_TYPE)}.  Returns JL_ERR_CAPACITY if an array is short. */
+typedef struct jl_log_record {
+    uint64_t offset;
+    uint64_t arena_off;
+    uint64_t size;
+} jl_log_record;
+typedef struct jl_log_report {
+    uint64_t bytes;
+    uint32_t reason;
+    uint32_t aux;
+} jl_log_report;
+
+#define JL_REASON_BAD_LENGTH 1      /* "bad record length"                       */
+#define JL_REASON_CHECKSUM 2        /* "checksum mismatch"                       */
+#define JL_REASON_PARTIAL_1 3       /* "partial record without end(1)"           */
+#define JL_REASON_PARTIAL_2 4       /* "partial record without end(2)"           */
+#define JL_REASON_MISSING_START_1 5 /* "missing start of fragmented record(1)"   */
+#define JL_REASON_MISSING_START_2 6 /* "missing start of fragmented record(2)"   */
+#define JL_REASON_MIDDLE_ERROR 7    /* "error in middle of record"               */
+#define JL_REASON_UNKNOWN_TYPE 8    /* "unknown record type N"                   */
+
+int jl_log_read_records(const uint8_t *log, uint64_t log_bytes, int checksum, uint64_t initial_offset,
+                        uint8_t *arena, uint64_t arena_cap, jl_log_record *records, uint64_t rec_cap,
+                        uint64_t *n_records, jl_log_report *reports, uint64_t rep_cap, uint64_t *n_reports);
+
+/* Batched LogWriter.emitPhysicalRecord headers (J/db/LogWriter.java:136-161):
+ * for fragment i (payload d_base[d_off[i], +d_len[i]), d_len[i] <= 0xffff,
+ * record type d_type[i]) writes [LE32 mask(extend(typeCrc[t], payload))][LE16 len][type]
+ * to d_header[7*i].  Framing (fragment boundaries, trailers) stays with the
+ * caller, as in LogWriter.addRecord. */
+int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint8_t *d_type,
+                       uint64_t n, uint8_t *d_header, void *stream);
+
+/* ------------------------------------------------------------ bench helpers */
+/* Fills d_dst[0, bytes) with the splitmix64 stream used by the benches
+ * (word i = splitmix64(seed + (first_word + i + 1) * golden)), on device. */
+int jl_fill_random_dev(void *d_dst, uint64_t bytes, uint64_t seed, uint64_t first_word, void *stream);
+
+/* Read-only HBM stream over d_src[0, bytes) (bytes % 16 == 0), XOR-folded into
+ * *d_sink: the measured read-bandwidth ceiling the roofline is quoted against. */
+int jl_read_stream_dev(const void *d_src, uint64_t bytes, uint32_t *d_sink, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JLCRC_H */

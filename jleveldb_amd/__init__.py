@@ -1,0 +1,350 @@
+"""jleveldb_amd — MI355X-native masked-CRC32C engine for jleveldb's checksum path.
+
+Python host layer over the C-ABI in ``include/jlcrc.h`` (``libjlcrc.so``, built
+in-tree from ``jleveldb_amd/csrc``).  It mirrors the reference's checksum
+surface, ``com.tchaicatkovsky.jleveldb.util.Crc32C``
+(src/main/java/com/tchaicatkovsky/jleveldb/util/Crc32C.java:29-167), and adds the
+batched device entry points used by the table/log shims.
+
+PyTorch is used only as device-memory / stream plumbing for the ``*_dev``
+helpers; the computation is the HIP engine.  There is no CPU fallback: if the
+shared library or a GPU is missing, the batch functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjlcrc.so")
+
+FLAG_MASK = 1
+
+# jl_log_event kinds (include/jlcrc.h)
+LOG_OK, LOG_BAD_CRC, LOG_BAD_LENGTH, LOG_ZERO_SKIP, LOG_EOF_BAD_LENGTH, LOG_EOF_TRUNC = 1, 2, 3, 4, 5, 6
+LOG_EVENT_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("type", "u1"), ("kind", "u1"), ("pad", "<u2")])
+LOG_RECORD_DTYPE = np.dtype([("offset", "<u8"), ("arena_off", "<u8"), ("size", "<u8")])
+LOG_REPORT_DTYPE = np.dtype([("bytes", "<u8"), ("reason", "<u4"), ("aux", "<u4")])
+
+# JL_REASON_* (include/jlcrc.h) -> the reference's Status messages (J/db/LogReader.java)
+REASONS = {
+    1: "bad record length",
+    2: "checksum mismatch",
+    3: "partial record without end(1)",
+    4: "partial record without end(2)",
+    5: "missing start of fragmented record(1)",
+    6: "missing start of fragmented record(2)",
+    7: "error in middle of record",
+    8: "unknown record type",
+}
+
+
+class JLError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compiles libjlcrc.so in-tree (hipcc, gfx950)."""
+    import subprocess
+
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc"), "-j4"], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise JLError(f"{LIB_PATH} is missing: build it with `make -C jleveldb_amd/csrc` (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u8, u32, u64, i32, sz = (ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                                 ctypes.c_size_t)
+    sig = {
+        "jl_crc32c_value": (u32, [vp, sz]),
+        "jl_crc32c_extend": (u32, [u32, vp, sz]),
+        "jl_crc32c_update": (u32, [u32, vp, sz]),
+        "jl_crc32c_mask": (u32, [u32]),
+        "jl_crc32c_unmask": (u32, [u32]),
+        "jl_init": (i32, [i32]),
+        "jl_shutdown": (i32, []),
+        "jl_last_error": (ctypes.c_char_p, []),
+        "jl_device_count": (i32, []),
+        "jl_version": (ctypes.c_char_p, []),
+        "jl_crc32c_fixed_dev": (i32, [vp, u64, u64, u32, vp, vp]),
+        "jl_crc32c_batch_dev": (i32, [vp, vp, vp, vp, vp, u64, u32, vp, vp]),
+        "jl_crc32c_batch": (i32, [vp, u64, vp, vp, vp, vp, u64, u32, vp]),
+        "jl_table_trailers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
+        "jl_table_verify_dev": (i32, [vp, vp, vp, u64, vp, vp]),
+        "jl_table_verify": (i32, [vp, u64, vp, vp, u64, vp]),
+        "jl_log_verify_dev": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64), vp]),
+        "jl_log_verify": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64)]),
+        "jl_log_read_records": (i32, [vp, u64, i32, u64, vp, u64, vp, u64, ctypes.POINTER(u64), vp, u64,
+                                      ctypes.POINTER(u64)]),
+        "jl_log_headers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
+        "jl_fill_random_dev": (i32, [vp, u64, u64, u64, vp]),
+        "jl_read_stream_dev": (i32, [vp, u64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    del u8
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().jl_last_error()
+        raise JLError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def _host(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+# --------------------------------------------------------------------------
+# Crc32C mirror (J/util/Crc32C.java)
+# --------------------------------------------------------------------------
+class Crc32C:
+    """Mirror of ``com.tchaicatkovsky.jleveldb.util.Crc32C``.
+
+    Statics ``value``/``extend``/``mask``/``unmask`` (Crc32C.java:43-93) and the
+    ``java.util.zip.Checksum`` instance API (:96-167) map onto the C-ABI's host
+    scalar entry points; batched work goes through the ``*_dev`` / batch
+    functions of this module.
+    """
+
+    kMaskDelta = 0xA282EAD8
+
+    def __init__(self) -> None:
+        self.reset()
+
+    # -- statics
+    @staticmethod
+    def value(data, offset: int = 0, n: int | None = None) -> int:
+        a = _host(data)
+        n = a.size - offset if n is None else n
+        if offset < 0 or n < 0 or offset + n > a.size:
+            raise IndexError("ArrayIndexOutOfBoundsException")
+        return lib().jl_crc32c_value(a.ctypes.data + offset, n)
+
+    @staticmethod
+    def extend(init_crc: int, data, offset: int = 0, n: int | None = None) -> int:
+        a = _host(data)
+        n = a.size - offset if n is None else n
+        if offset < 0 or n < 0 or offset + n > a.size:
+            raise IndexError("ArrayIndexOutOfBoundsException")
+        return lib().jl_crc32c_extend(init_crc & 0xFFFFFFFF, a.ctypes.data + offset, n)
+
+    @staticmethod
+    def mask(crc: int) -> int:
+        return lib().jl_crc32c_mask(crc & 0xFFFFFFFF)
+
+    @staticmethod
+    def unmask(masked_crc: int) -> int:
+        return lib().jl_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+    # -- java.util.zip.Checksum
+    def reset(self) -> None:
+        self._crc = 0xFFFFFFFF
+
+    def setValue(self, v: int) -> None:  # noqa: N802 (reference name)
+        self._crc = (~v) & 0xFFFFFFFF
+
+    def getValue(self) -> int:  # noqa: N802
+        return (~self._crc) & 0xFFFFFFFF
+
+    def update(self, b, off: int | None = None, length: int | None = None) -> None:
+        if isinstance(b, int) and off is None:  # update(int b), Crc32C.java:165-167
+            one = np.array([b & 0xFF], dtype=np.uint8)
+            self._crc = lib().jl_crc32c_update(self._crc, one.ctypes.data, 1)
+            return
+        a = _host(b)
+        off = 0 if off is None else off
+        length = a.size - off if length is None else length
+        if off < 0 or length < 0 or off + length > a.size:
+            raise IndexError("ArrayIndexOutOfBoundsException")
+        self._crc = lib().jl_crc32c_update(self._crc, a.ctypes.data + off, length)
+
+
+# --------------------------------------------------------------------------
+# device engine
+# --------------------------------------------------------------------------
+def init(device: int = 0) -> None:
+    _check(lib().jl_init(device), "jl_init")
+
+
+def shutdown() -> None:
+    _check(lib().jl_shutdown(), "jl_shutdown")
+
+
+def version() -> str:
+    return lib().jl_version().decode()
+
+
+def _dptr(t) -> int:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise JLError("expected a device tensor")
+    if not t.is_contiguous():
+        raise JLError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _stream(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def crc32c_fixed_dev(data, block_bytes: int, n_blocks: int | None = None, flags: int = FLAG_MASK, out=None,
+                     stream=None):
+    """Per-block (masked) CRC32C of contiguous blocks in a uint8 device tensor."""
+    import torch
+
+    n_blocks = data.numel() // block_bytes if n_blocks is None else n_blocks
+    if n_blocks * block_bytes > data.numel():
+        raise JLError("blocks exceed the tensor")
+    if out is None:
+        out = torch.empty(n_blocks, dtype=torch.int32, device=data.device)
+    _check(lib().jl_crc32c_fixed_dev(_dptr(data), block_bytes, n_blocks, flags, _dptr(out), _stream(stream)),
+           "jl_crc32c_fixed_dev")
+    return out
+
+
+def crc32c_batch_dev(base, off, length, init=None, suffix=None, flags: int = FLAG_MASK, out=None, stream=None):
+    """Per-block (masked) CRC32C of arena ranges (device tensors: u8 base, i64 off, i32 len)."""
+    import torch
+
+    n = off.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=base.device)
+    _check(lib().jl_crc32c_batch_dev(_dptr(base), _dptr(off), _dptr(length), _dptr(init), _dptr(suffix), n, flags,
+                                     _dptr(out), _stream(stream)), "jl_crc32c_batch_dev")
+    return out
+
+
+def crc32c_batch(base, off, length, init=None, suffix=None, flags: int = FLAG_MASK) -> np.ndarray:
+    """Host-memory batch (numpy): stages to the device, returns uint32 results."""
+    b = _host(base)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    init_a = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+    sfx_a = None if suffix is None else np.ascontiguousarray(suffix, dtype=np.uint8)
+    out = np.zeros(off.size, dtype=np.uint32)
+    _check(lib().jl_crc32c_batch(b.ctypes.data, b.size, off.ctypes.data, length.ctypes.data,
+                                 None if init_a is None else init_a.ctypes.data,
+                                 None if sfx_a is None else sfx_a.ctypes.data, off.size, flags, out.ctypes.data),
+           "jl_crc32c_batch")
+    return out
+
+
+def table_verify(file, off, size) -> np.ndarray:
+    """Batched TableFormat.readBlock checksum test over a host file image (1 = ok)."""
+    f = _host(file)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    size = np.ascontiguousarray(size, dtype=np.uint32)
+    st = np.zeros(off.size, dtype=np.uint8)
+    _check(lib().jl_table_verify(f.ctypes.data, f.size, off.ctypes.data, size.ctypes.data, off.size, st.ctypes.data),
+           "jl_table_verify")
+    return st
+
+
+def table_verify_dev(file, off, size, out=None, stream=None):
+    import torch
+
+    n = off.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint8, device=file.device)
+    _check(lib().jl_table_verify_dev(_dptr(file), _dptr(off), _dptr(size), n, _dptr(out), _stream(stream)),
+           "jl_table_verify_dev")
+    return out
+
+
+def table_trailers_dev(file, off, size, types=None, out=None, stream=None):
+    import torch
+
+    n = off.numel()
+    if out is None:
+        out = torch.empty(5 * n, dtype=torch.uint8, device=file.device)
+    _check(lib().jl_table_trailers_dev(_dptr(file), _dptr(off), _dptr(size), _dptr(types), n, _dptr(out),
+                                       _stream(stream)), "jl_table_trailers_dev")
+    return out
+
+
+def log_headers_dev(base, off, length, types, out=None, stream=None):
+    import torch
+
+    n = off.numel()
+    if out is None:
+        out = torch.empty(7 * n, dtype=torch.uint8, device=base.device)
+    _check(lib().jl_log_headers_dev(_dptr(base), _dptr(off), _dptr(length), _dptr(types), n, _dptr(out),
+                                    _stream(stream)), "jl_log_headers_dev")
+    return out
+
+
+def log_verify(log, checksum: bool = True) -> np.ndarray:
+    """Device verification of a host log image -> physical-record events (LOG_EVENT_DTYPE)."""
+    a = _host(log)
+    cap = a.size // 7 + 2
+    ev = np.zeros(cap, dtype=LOG_EVENT_DTYPE)
+    n = ctypes.c_uint64(0)
+    _check(lib().jl_log_verify(a.ctypes.data if a.size else None, a.size, int(checksum), ev.ctypes.data, cap,
+                               ctypes.byref(n)), "jl_log_verify")
+    return ev[: n.value]
+
+
+def log_verify_dev(log, checksum: bool = True, events=None, stream=None):
+    """Device-resident verification; returns (events tensor view, count)."""
+    import torch
+
+    n = ctypes.c_uint64(0)
+    cap = 0 if events is None else events.numel() // LOG_EVENT_DTYPE.itemsize
+    rc = lib().jl_log_verify_dev(_dptr(log), log.numel(), int(checksum), _dptr(events), cap, ctypes.byref(n),
+                                 _stream(stream))
+    if rc == -5:  # JL_ERR_CAPACITY: allocate and retry
+        events = torch.empty(max(1, n.value) * LOG_EVENT_DTYPE.itemsize, dtype=torch.uint8, device=log.device)
+        rc = lib().jl_log_verify_dev(_dptr(log), log.numel(), int(checksum), _dptr(events), n.value, ctypes.byref(n),
+                                     _stream(stream))
+    _check(rc, "jl_log_verify_dev")
+    return events, n.value
+
+
+def log_read_records(log, checksum: bool = True, initial_offset: int = 0):
+    """LogReader.readRecord over a whole log image: ([(offset, bytes)], [(bytes, reason, aux)])."""
+    a = _host(log)
+    arena = np.zeros(max(a.size, 1), dtype=np.uint8)
+    cap = a.size // 7 + 2
+    recs = np.zeros(cap, dtype=LOG_RECORD_DTYPE)
+    reps = np.zeros(cap, dtype=LOG_REPORT_DTYPE)
+    nr, np_ = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(lib().jl_log_read_records(a.ctypes.data if a.size else None, a.size, int(checksum), initial_offset,
+                                     arena.ctypes.data, arena.size, recs.ctypes.data, cap, ctypes.byref(nr),
+                                     reps.ctypes.data, cap, ctypes.byref(np_)), "jl_log_read_records")
+    records = [(int(r["offset"]), arena[int(r["arena_off"]):int(r["arena_off"]) + int(r["size"])].tobytes())
+               for r in recs[: nr.value]]
+    reports = [(int(r["bytes"]), int(r["reason"]), int(r["aux"])) for r in reps[: np_.value]]
+    return records, reports
+
+
+def fill_random_dev(t, seed: int, first_word: int = 0, stream=None) -> None:
+    _check(lib().jl_fill_random_dev(_dptr(t), t.numel() * t.element_size(), seed & (2**64 - 1), first_word,
+                                    _stream(stream)), "jl_fill_random_dev")
+
+
+def read_stream_dev(t, sink, stream=None) -> None:
+    """Read-only HBM stream over a device tensor (roofline calibration)."""
+    _check(lib().jl_read_stream_dev(_dptr(t), t.numel() * t.element_size(), _dptr(sink), _stream(stream)),
+           "jl_read_stream_dev")

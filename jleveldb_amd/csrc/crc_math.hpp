@@ -1,0 +1,126 @@
+// crc_math.hpp — GF(2) algebra of the reflected CRC-32C state, used on the
+// host to build the device table images (jlcrc_api.hip) and by the host scalar
+// path (host_crc.cpp).
+//
+// State convention: `s` is the bit-flipped crc, exactly the Java field
+// `Crc32C.crc` (J/util/Crc32C.java:96): value() = ~update(~0, data).
+//   one data byte   : s' = (s >> 8) ^ T0[(s ^ b) & 0xff]        (Crc32C.java:165-167)
+//   one zero byte   : z(s) = (s >> 8) ^ T0[s & 0xff]            (linear over GF(2))
+//   T_k[i]          = z^k(T0[i])  — the reference's T8_k tables (Crc32C.java:173-334)
+//   slicing-by-4    : x = s ^ LE32(b0..b3);
+//                     s' = T3[x&ff] ^ T2[x>>8&ff] ^ T1[x>>16&ff] ^ T0[x>>24]
+// z is invertible (the top byte of T0[i] is a permutation of i), which gives the
+// exact "un-shift" z^-1 used by the device engine to re-align lane chains.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+namespace jlmath {
+
+constexpr uint32_t kPoly = 0x82F63B78u;  // reflected Castagnoli (Crc32C.java:169-171)
+constexpr uint32_t kMaskDelta = 0xa282ead8u;  // Crc32C.java:31
+
+struct Tables {
+    uint32_t t[8][256];     // T_0..T_7 (slicing-by-8, host path)
+    uint8_t inv_top[256];   // inv_top[T0[i] >> 24] = i
+    Tables() {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((c & 1u) ? kPoly : 0u);
+            t[0][i] = c;
+        }
+        for (int k = 1; k < 8; k++)
+            for (uint32_t i = 0; i < 256; i++) t[k][i] = (t[k - 1][i] >> 8) ^ t[0][t[k - 1][i] & 0xffu];
+        bool seen[256] = {false};
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t top = t[0][i] >> 24;
+            if (seen[top]) throw std::logic_error("CRC-32C table top byte is not a permutation");
+            seen[top] = true;
+            inv_top[top] = (uint8_t)i;
+        }
+    }
+    uint32_t z(uint32_t s) const { return (s >> 8) ^ t[0][s & 0xffu]; }
+    uint32_t zinv(uint32_t s) const {
+        uint32_t i = inv_top[s >> 24];
+        return ((s ^ t[0][i]) << 8) | i;
+    }
+    uint32_t zn(uint32_t s, uint64_t n) const {
+        for (uint64_t i = 0; i < n; i++) s = z(s);
+        return s;
+    }
+    uint32_t zinvn(uint32_t s, uint64_t n) const {
+        for (uint64_t i = 0; i < n; i++) s = zinv(s);
+        return s;
+    }
+};
+
+inline const Tables &tables() {
+    static const Tables T;
+    return T;
+}
+
+inline uint32_t mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + kMaskDelta; }
+inline uint32_t unmask(uint32_t m) {
+    uint32_t rot = m - kMaskDelta;
+    return (rot >> 17) | (rot << 15);
+}
+
+// ----------------------------------------------------------------------------
+// Device LDS image (160 KiB = the whole LDS of one CU), see DESIGN.md §3.
+//
+// The engine interleaves each 256-byte "step" of a block over the 64 lanes of a
+// wave (lane l owns the dword at 4*l), so lane l's chain visits words
+// 256*k + 4*l.  Each chain step therefore processes 4 data bytes followed by
+// 252 bytes that belong to other lanes; their contribution is added by the
+// other lanes, so the step table is the slicing-by-4 table shifted by 252 zero
+// bytes:  G_j[i] = z^(252+j)(T0[i]), byte 0 of x uses G_3 ... byte 3 uses G_0.
+//
+// Region A (128 KiB): G_0..G_3 replicated 32x so that lane l always reads LDS
+//   bank (l & 31): dword index ((t*256 + i)*32 + b).  ds_read_b32 serves lanes
+//   0-31 and 32-63 in separate cycles, so 32 copies make every lookup
+//   conflict-free.
+// Region B (32 KiB): per-lane re-alignment tables.  After its last step lane l
+//   sits 4*l bytes past the end of the block, so its state is corrected with
+//   z^-(4*l), applied as 8 nibble lookups:  N_{l,j}[v] = z^-(4l)(v << 4j),
+//   dword index 32768 + (((l>>5)*8 + j)*16 + v)*32 + (l & 31).
+// ----------------------------------------------------------------------------
+constexpr int kGapBytes = 252;
+constexpr size_t kImageDwords = 32768 + 8192;
+constexpr size_t kImageBytes = kImageDwords * 4;  // 163840
+
+inline std::vector<uint32_t> build_lds_image() {
+    const Tables &T = tables();
+    std::vector<uint32_t> img(kImageDwords);
+    for (int t = 0; t < 4; t++)
+        for (int i = 0; i < 256; i++) {
+            uint32_t g = T.zn(T.t[0][i], (uint64_t)kGapBytes + t);
+            for (int b = 0; b < 32; b++) img[((size_t)t * 256 + i) * 32 + b] = g;
+        }
+    for (int l = 0; l < 64; l++)
+        for (int j = 0; j < 8; j++)
+            for (int v = 0; v < 16; v++) {
+                uint32_t c = T.zinvn((uint32_t)v << (4 * j), 4u * (uint32_t)l);
+                img[32768 + ((size_t)((l >> 5) * 8 + j) * 16 + v) * 32 + (l & 31)] = c;
+            }
+    return img;
+}
+
+// Small global-memory table used by the kernels' scalar epilogues:
+//   [0,256)   T0
+//   [256,512) inv_top (as u32)
+//   [512,517) typeCrc[0..4] = value([t])  (LogWriter.initTypeCrc, J/db/LogWriter.java:51-57)
+constexpr size_t kAuxDwords = 520;
+inline std::vector<uint32_t> build_aux() {
+    const Tables &T = tables();
+    std::vector<uint32_t> aux(kAuxDwords, 0);
+    for (int i = 0; i < 256; i++) {
+        aux[i] = T.t[0][i];
+        aux[256 + i] = T.inv_top[i];
+    }
+    for (uint32_t t = 0; t < 5; t++) aux[512 + t] = ~((0xffffffffu >> 8) ^ T.t[0][(0xffffffffu ^ t) & 0xffu]);
+    return aux;
+}
+
+}  // namespace jlmath

@@ -1,0 +1,412 @@
+// jlcrc_api.hip — C-ABI of the engine (include/jlcrc.h): device context,
+// launches, host staging and the caller shims for the four reference call sites.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jlcrc.h"
+#include "crc_math.hpp"
+#include "jlcrc_kernels.hpp"
+
+static_assert(jlmath::kImageBytes == jlk::kImageBytes, "LDS image size mismatch");
+static_assert(sizeof(jl_log_event) == sizeof(jlk::LogEvent), "event layout mismatch");
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define JL_HIP(call)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (call);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            return fail(JL_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));               \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Context {
+    std::mutex mu;  // guards init and the staging workspace of the host-memory entry points
+    bool ready = false;
+    int device = -1;
+    int cus = 0;
+    hipStream_t stream = nullptr;
+    void *d_img = nullptr;   // 160 KiB LDS image
+    uint32_t *d_aux = nullptr;
+    uint8_t *d_zero = nullptr;  // 4 KiB of zeros
+    // staging workspace (host-memory APIs, log verify)
+    DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp;
+};
+
+Context &ctx() {
+    static Context c;
+    return c;
+}
+
+int ensure_ready() {
+    Context &c = ctx();
+    if (c.ready) return JL_OK;
+    int r = jl_init(0);
+    return r;
+}
+
+hipStream_t pick(void *stream) { return stream ? (hipStream_t)stream : ctx().stream; }
+
+int grid_for(uint64_t blocks) {
+    // one 1024-thread workgroup (16 waves) per CU; fewer when there is little work
+    uint64_t wg = (blocks + 15) / 16;
+    int cus = ctx().cus;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(wg, (uint64_t)cus));
+}
+
+jlk::KParams base_params(const void *d_base, uint64_t n, int mode) {
+    jlk::KParams P;
+    memset(&P, 0, sizeof(P));
+    P.base = (const uint8_t *)d_base;
+    P.aux = ctx().d_aux;
+    P.zero = ctx().d_zero;
+    P.n = n;
+    P.mode = mode;
+    return P;
+}
+
+int run_general(const jlk::KParams &P, hipStream_t st) {
+    if (P.n == 0) return JL_OK;
+    JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
+    return JL_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *jl_last_error(void) { return g_err.c_str(); }
+
+const char *jl_version(void) { return "jlcrc 0.1 gfx950 (lane-interleaved slicing-by-4, LDS gap tables)"; }
+
+int jl_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int jl_init(int device) {
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.ready) {
+        if (c.device == device) return JL_OK;
+        return fail(JL_ERR_INVALID, "jl_init: engine already bound to device " + std::to_string(c.device));
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(JL_ERR_NO_DEVICE, "jl_init: no HIP device");
+    if (device < 0 || device >= n) return fail(JL_ERR_INVALID, "jl_init: bad device ordinal");
+    JL_HIP(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    JL_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+        return fail(JL_ERR_NO_DEVICE, std::string("jl_init: engine is built for gfx950, device is ") + prop.gcnArchName);
+    c.cus = prop.multiProcessorCount;
+    JL_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    std::vector<uint32_t> img = jlmath::build_lds_image();
+    std::vector<uint32_t> aux = jlmath::build_aux();
+    JL_HIP(hipMalloc(&c.d_img, jlmath::kImageBytes));
+    JL_HIP(hipMalloc((void **)&c.d_aux, aux.size() * 4));
+    JL_HIP(hipMalloc((void **)&c.d_zero, 4096));
+    JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
+    JL_HIP(hipMemcpy(c.d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice));
+    JL_HIP(hipMemset(c.d_zero, 0, 4096));
+    c.device = device;
+    c.ready = true;
+    return JL_OK;
+}
+
+int jl_shutdown(void) {
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.ready) return JL_OK;
+    (void)hipSetDevice(c.device);
+    (void)hipStreamSynchronize(c.stream);
+    for (DevBuf *b : {&c.ws_data, &c.ws_off, &c.ws_len, &c.ws_init, &c.ws_sfx, &c.ws_out, &c.ws_cnt, &c.ws_start,
+                      &c.ws_ev, &c.ws_ok, &c.ws_tmp})
+        b->release();
+    (void)hipFree(c.d_img);
+    (void)hipFree(c.d_aux);
+    (void)hipFree(c.d_zero);
+    (void)hipStreamDestroy(c.stream);
+    c.d_img = nullptr;
+    c.d_aux = nullptr;
+    c.d_zero = nullptr;
+    c.stream = nullptr;
+    c.ready = false;
+    c.device = -1;
+    return JL_OK;
+}
+
+// ----------------------------------------------------------- batch checksums
+int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags,
+                        uint32_t *d_out, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n_blocks == 0) return JL_OK;
+    if (!d_data || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: null pointer");
+    if (block_bytes > 0xffffffffull) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: block_bytes >= 4 GiB");
+    hipStream_t st = pick(stream);
+    if (block_bytes == 4096) {
+        static const int nt = [] {
+            const char *e = getenv("JL_FIXED_NT");
+            return e ? atoi(e) : 1;
+        }();
+        JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
+                                   grid_for(n_blocks), nt, st));
+        return JL_OK;
+    }
+    jlk::KParams P = base_params(d_data, n_blocks, jlk::MODE_CRC);
+    P.fixed_bytes = block_bytes;
+    P.flags = flags;
+    P.out32 = d_out;
+    return run_general(P, st);
+}
+
+int jl_crc32c_batch_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint32_t *d_init,
+                        const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!d_base || !d_off || !d_len || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_batch_dev: null pointer");
+    jlk::KParams P = base_params(d_base, n, jlk::MODE_CRC);
+    P.off = d_off;
+    P.len = d_len;
+    P.init = d_init;
+    P.suffix = d_suffix;
+    P.flags = flags;
+    P.out32 = d_out;
+    return run_general(P, pick(stream));
+}
+
+int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *off, const uint32_t *len,
+                    const uint32_t *init, const uint8_t *suffix, uint64_t n, uint32_t flags, uint32_t *out) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!base || !off || !len || !out) return fail(JL_ERR_INVALID, "jl_crc32c_batch: null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] + (uint64_t)len[i] > base_bytes) return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    hipStream_t st = c.stream;
+    JL_HIP(c.ws_data.ensure(base_bytes + 16));
+    JL_HIP(c.ws_off.ensure(n * 8));
+    JL_HIP(c.ws_len.ensure(n * 4));
+    JL_HIP(c.ws_out.ensure(n * 4));
+    JL_HIP(hipMemcpyAsync(c.ws_data.p, base, base_bytes, hipMemcpyHostToDevice, st));
+    JL_HIP(hipMemcpyAsync(c.ws_off.p, off, n * 8, hipMemcpyHostToDevice, st));
+    JL_HIP(hipMemcpyAsync(c.ws_len.p, len, n * 4, hipMemcpyHostToDevice, st));
+    jlk::KParams P = base_params(c.ws_data.p, n, jlk::MODE_CRC);
+    P.off = (const uint64_t *)c.ws_off.p;
+    P.len = (const uint32_t *)c.ws_len.p;
+    if (init) {
+        JL_HIP(c.ws_init.ensure(n * 4));
+        JL_HIP(hipMemcpyAsync(c.ws_init.p, init, n * 4, hipMemcpyHostToDevice, st));
+        P.init = (const uint32_t *)c.ws_init.p;
+    }
+    if (suffix) {
+        JL_HIP(c.ws_sfx.ensure(n));
+        JL_HIP(hipMemcpyAsync(c.ws_sfx.p, suffix, n, hipMemcpyHostToDevice, st));
+        P.suffix = (const uint8_t *)c.ws_sfx.p;
+    }
+    P.flags = flags;
+    P.out32 = (uint32_t *)c.ws_out.p;
+    if (int r = run_general(P, st)) return r;
+    JL_HIP(hipMemcpyAsync(out, c.ws_out.p, n * 4, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipStreamSynchronize(st));
+    return JL_OK;
+}
+
+// ------------------------------------------------------------- table shims
+int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, const uint8_t *d_type,
+                          uint64_t n, uint8_t *d_trailer, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!d_file || !d_off || !d_size || !d_trailer) return fail(JL_ERR_INVALID, "jl_table_trailers_dev: null pointer");
+    jlk::KParams P = base_params(d_file, n, jlk::MODE_TRAILER);
+    P.off = d_off;
+    P.len = d_size;
+    P.type = d_type;
+    P.out8 = d_trailer;
+    return run_general(P, pick(stream));
+}
+
+int jl_table_verify_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, uint64_t n,
+                        uint8_t *d_status, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!d_file || !d_off || !d_size || !d_status) return fail(JL_ERR_INVALID, "jl_table_verify_dev: null pointer");
+    jlk::KParams P = base_params(d_file, n, jlk::MODE_TABLE_VERIFY);
+    P.off = d_off;
+    P.len = d_size;
+    P.len_add = 1;  // block || type byte
+    P.out8 = d_status;
+    return run_general(P, pick(stream));
+}
+
+int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *off, const uint32_t *size, uint64_t n,
+                    uint8_t *status) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!file || !off || !size || !status) return fail(JL_ERR_INVALID, "jl_table_verify: null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] + (uint64_t)size[i] + 5 > file_bytes)
+            return fail(JL_ERR_INVALID, "jl_table_verify: truncated block read");  // TableFormat.java:203-206
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    hipStream_t st = c.stream;
+    JL_HIP(c.ws_data.ensure(file_bytes + 16));
+    JL_HIP(c.ws_off.ensure(n * 8));
+    JL_HIP(c.ws_len.ensure(n * 4));
+    JL_HIP(c.ws_ok.ensure(n));
+    JL_HIP(hipMemcpyAsync(c.ws_data.p, file, file_bytes, hipMemcpyHostToDevice, st));
+    JL_HIP(hipMemcpyAsync(c.ws_off.p, off, n * 8, hipMemcpyHostToDevice, st));
+    JL_HIP(hipMemcpyAsync(c.ws_len.p, size, n * 4, hipMemcpyHostToDevice, st));
+    jlk::KParams P = base_params(c.ws_data.p, n, jlk::MODE_TABLE_VERIFY);
+    P.off = (const uint64_t *)c.ws_off.p;
+    P.len = (const uint32_t *)c.ws_len.p;
+    P.len_add = 1;
+    P.out8 = (uint8_t *)c.ws_ok.p;
+    if (int r = run_general(P, st)) return r;
+    JL_HIP(hipMemcpyAsync(status, c.ws_ok.p, n, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipStreamSynchronize(st));
+    return JL_OK;
+}
+
+// --------------------------------------------------------------- log shims
+int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint8_t *d_type,
+                       uint64_t n, uint8_t *d_header, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n == 0) return JL_OK;
+    if (!d_base || !d_off || !d_len || !d_type || !d_header)
+        return fail(JL_ERR_INVALID, "jl_log_headers_dev: null pointer");
+    jlk::KParams P = base_params(d_base, n, jlk::MODE_LOG_HEADER);
+    P.off = d_off;
+    P.len = d_len;
+    P.type = d_type;
+    P.out8 = d_header;
+    return run_general(P, pick(stream));
+}
+
+static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
+                           uint64_t *n_events, hipStream_t st) {
+    Context &c = ctx();
+    const uint64_t nb = (log_bytes + 32767) / 32768;
+    *n_events = 0;
+    if (nb == 0) return JL_OK;
+    JL_HIP(c.ws_cnt.ensure(nb * 8));
+    JL_HIP(c.ws_start.ensure(nb * 8));
+    uint64_t *cnt = (uint64_t *)c.ws_cnt.p, *start = (uint64_t *)c.ws_start.p;
+    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 0, cnt, nullptr, nullptr, nullptr, nullptr, st));
+    size_t tmp = 0;
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, start, (int)nb, st));
+    JL_HIP(c.ws_tmp.ensure(tmp));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, tmp, cnt, start, (int)nb, st));
+    uint64_t last_start = 0, last_cnt = 0;
+    JL_HIP(hipMemcpyAsync(&last_start, start + nb - 1, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipMemcpyAsync(&last_cnt, cnt + nb - 1, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipStreamSynchronize(st));
+    const uint64_t total = last_start + last_cnt;
+    *n_events = total;
+    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    if (total == 0) return JL_OK;
+    JL_HIP(c.ws_off.ensure(total * 8));
+    JL_HIP(c.ws_len.ensure(total * 4));
+    JL_HIP(c.ws_ok.ensure(total));
+    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 1, cnt, start, (jlk::LogEvent *)d_events,
+                                (uint64_t *)c.ws_off.p, (uint32_t *)c.ws_len.p, st));
+    if (checksum) {
+        jlk::KParams P = base_params(d_log, total, jlk::MODE_LOG_VERIFY);
+        P.off = (const uint64_t *)c.ws_off.p;
+        P.len = (const uint32_t *)c.ws_len.p;
+        P.out8 = (uint8_t *)c.ws_ok.p;
+        if (int r = run_general(P, st)) return r;
+        JL_HIP(jlk::launch_log_finalize(nb, start, cnt, (const uint8_t *)c.ws_ok.p, (jlk::LogEvent *)d_events, 1, st));
+    }
+    JL_HIP(hipStreamSynchronize(st));
+    return JL_OK;
+}
+
+int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
+                      uint64_t *n_events, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (!n_events || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev: null pointer");
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);  // shares the walk workspace
+    return log_verify_impl(d_log, log_bytes, checksum, d_events, cap, n_events, pick(stream));
+}
+
+int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_event *events, uint64_t cap,
+                  uint64_t *n_events) {
+    if (int r = ensure_ready()) return r;
+    if (!n_events || (log_bytes && !log)) return fail(JL_ERR_INVALID, "jl_log_verify: null pointer");
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    hipStream_t st = c.stream;
+    *n_events = 0;
+    if (log_bytes == 0) return JL_OK;
+    JL_HIP(c.ws_data.ensure(log_bytes + 16));
+    JL_HIP(hipMemcpyAsync(c.ws_data.p, log, log_bytes, hipMemcpyHostToDevice, st));
+    // events land in ws_ev, then copy out
+    const uint64_t ev_cap = log_bytes / 7 + 2;  // upper bound on physical records
+    JL_HIP(c.ws_ev.ensure(ev_cap * sizeof(jl_log_event)));
+    uint64_t total = 0;
+    int r = log_verify_impl(c.ws_data.p, log_bytes, checksum, (jl_log_event *)c.ws_ev.p, ev_cap, &total, st);
+    *n_events = total;
+    if (r) return r;
+    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    if (total) {
+        JL_HIP(hipMemcpyAsync(events, c.ws_ev.p, total * sizeof(jl_log_event), hipMemcpyDeviceToHost, st));
+        JL_HIP(hipStreamSynchronize(st));
+    }
+    return JL_OK;
+}
+
+// ------------------------------------------------------------------ helpers
+int jl_fill_random_dev(void *d_dst, uint64_t bytes, uint64_t seed, uint64_t first_word, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (bytes == 0) return JL_OK;
+    if (!d_dst) return fail(JL_ERR_INVALID, "jl_fill_random_dev: null pointer");
+    JL_HIP(jlk::launch_fill_random(d_dst, bytes, seed, first_word, pick(stream)));
+    return JL_OK;
+}
+
+int jl_read_stream_dev(const void *d_src, uint64_t bytes, uint32_t *d_sink, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (!d_src || !d_sink || bytes % 16) return fail(JL_ERR_INVALID, "jl_read_stream_dev: bad arguments");
+    JL_HIP(jlk::launch_read_stream(d_src, bytes, d_sink, ctx().cus * 8, pick(stream)));
+    return JL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,55 @@
+// jlcrc_kernels.hpp — launch interface between the C-ABI (jlcrc_api.hip) and the
+// device kernels (jlcrc_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace jlk {
+
+constexpr uint32_t kImageBytes = 163840;  // must equal jlmath::kImageBytes
+
+enum : int {
+    MODE_CRC = 0,           // out32[i] = crc / mask(crc)
+    MODE_TABLE_VERIFY = 1,  // out8[i] = (LE32 @ ptr+n == mask(crc))   TableFormat.readBlock
+    MODE_LOG_VERIFY = 2,    // out8[i] = (LE32 @ ptr-6 == mask(crc))   LogReader.readPhysicalRecord
+    MODE_TRAILER = 3,       // out8[5i..] = [type][LE32 mask]          TableBuilder.writeRawBlock
+    MODE_LOG_HEADER = 4,    // out8[7i..] = [LE32 mask][LE16 n][type]  LogWriter.emitPhysicalRecord
+};
+
+struct KParams {
+    const uint8_t *base;     // arena
+    const uint64_t *off;     // per-block offsets (null = fixed stride)
+    const uint32_t *len;     // per-block lengths
+    uint32_t len_add;        // added to len[i] (table verify covers size+1 bytes)
+    uint64_t fixed_bytes;    // stride/length when off == null
+    const uint32_t *init;    // optional per-block extend() init
+    const uint8_t *suffix;   // optional per-block suffix byte
+    const uint8_t *type;     // record / compression type (trailer, log header)
+    const uint32_t *aux;     // T0, inv_top, typeCrc (crc_math.hpp build_aux)
+    const uint8_t *zero;     // 4 KiB of zeros: target of predicated-off loads
+    uint64_t n;              // blocks
+    uint32_t flags;          // JL_FLAG_MASK
+    int mode;
+    uint32_t *out32;
+    uint8_t *out8;
+};
+
+struct LogEvent {  // layout-identical to jl_log_event
+    uint64_t offset;
+    uint32_t length;
+    uint8_t type;
+    uint8_t kind;
+    uint16_t pad;
+};
+
+hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
+                          uint32_t flags, uint32_t *out, int grid, int nt, hipStream_t st);
+hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
+hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
+                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st);
+hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
+                               LogEvent *ev, int checksum, hipStream_t st);
+hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st);
+hipError_t launch_fill_random(void *dst, uint64_t bytes, uint64_t seed, uint64_t first_word, hipStream_t st);
+
+}  // namespace jlk

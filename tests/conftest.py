@@ -1,0 +1,56 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; parity tests of the HIP engine")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as o
+
+    o.build()
+    return o
+
+
+@pytest.fixture(scope="session")
+def jl():
+    import jleveldb_amd
+
+    jleveldb_amd.build()
+    return jleveldb_amd
+
+
+@pytest.fixture(scope="session")
+def gpu(jl):
+    """Initialises the engine on cuda:0 (fails loudly: the product has no CPU path)."""
+    import torch
+
+    assert torch.cuda.is_available(), "GPU test collected on a machine without a GPU"
+    torch.cuda.set_device(0)
+    jl.init(0)
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    d = os.path.join(ROOT, "tests", "golden")
+
+    def load(name):
+        p = os.path.join(d, name)
+        if name.endswith(".json"):
+            with open(p) as f:
+                return json.load(f)
+        with open(p, "rb") as f:
+            return f.read()
+
+    return load

@@ -1,0 +1,68 @@
+// Host emulation of the device engine's per-lane algorithm (test only): checks
+// the LDS image math (gap tables, per-lane z^-(4l) re-alignment, front
+// injection z^-r(~init)) against a plain byte-serial CRC-32C.
+#include "../../jleveldb_amd/csrc/crc_math.hpp"
+#include <cstdio>
+#include <random>
+using namespace jlmath;
+
+static uint32_t ref_update(uint32_t s, const uint8_t* p, size_t n) {
+    const Tables& T = tables();
+    for (size_t i = 0; i < n; i++) s = (s >> 8) ^ T.t[0][(s ^ p[i]) & 0xff];
+    return s;
+}
+
+static uint32_t emulate(const std::vector<uint32_t>& img, const uint8_t* base, uint32_t n, uint32_t init) {
+    const Tables& T = tables();
+    uint32_t s0 = ~init;
+    if (n == 0) return ~s0;
+    uint32_t K = (n + 255) / 256, f = 256 * K - n, l0 = f >> 2, r = f & 3;
+    uint32_t inj = T.zinvn(s0, r);
+    uint32_t total = 0;
+    for (int lane = 0; lane < 64; lane++) {
+        uint32_t s = 0;
+        for (uint32_t k = 0; k < K; k++) {
+            int64_t p = 256 * (int64_t)k + 4 * lane - f;
+            uint32_t w = 0;
+            if (p >= 0) memcpy(&w, base + p, 4);
+            else if (p > -4) { for (int j = 0; j < 4 + p; j++) w |= (uint32_t)base[j] << (8 * (j - p)); }
+            if (k == 0 && (uint32_t)lane == l0) s = inj;
+            uint32_t x = s ^ w;
+            uint32_t b = lane & 31;
+            s = img[((3 * 256) + (x & 0xff)) * 32 + b] ^ img[((2 * 256) + ((x >> 8) & 0xff)) * 32 + b] ^
+                img[((1 * 256) + ((x >> 16) & 0xff)) * 32 + b] ^ img[((0 * 256) + (x >> 24)) * 32 + b];
+        }
+        uint32_t c = 0;
+        for (int j = 0; j < 8; j++) {
+            uint32_t v = (s >> (4 * j)) & 15;
+            c ^= img[32768 + (((lane >> 5) * 8 + j) * 16 + v) * 32 + (lane & 31)];
+        }
+        total ^= c;
+    }
+    return ~total;
+}
+
+int main() {
+    auto img = build_lds_image();
+    std::mt19937_64 rng(42);
+    std::vector<uint8_t> buf(70000 + 16);
+    for (auto& b : buf) b = (uint8_t)rng();
+    int bad = 0, cases = 0;
+    for (uint32_t n = 0; n <= 1300; n++) {
+        for (int a = 0; a < 4; a++) {
+            uint32_t init = (n % 3 == 0) ? 0 : (uint32_t)rng();
+            uint32_t want = ~ref_update(~init, buf.data() + a, n);
+            uint32_t got = emulate(img, buf.data() + a, n, init);
+            cases++;
+            if (want != got && bad++ < 5) printf("mismatch n=%u a=%d %08x %08x\n", n, a, want, got);
+        }
+    }
+    for (uint32_t n : {4096u, 4097u, 8191u, 65536u, 65535u, 32768u, 65000u}) {
+        uint32_t want = ~ref_update(~0u, buf.data() + 1, n);
+        uint32_t got = emulate(img, buf.data() + 1, n, 0);
+        cases++;
+        if (want != got && bad++ < 10) printf("mismatch n=%u %08x %08x\n", n, want, got);
+    }
+    printf("%d cases, %d mismatches\n", cases, bad);
+    return bad != 0;
+}
