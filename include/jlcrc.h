@@ -10,8 +10,8 @@
  *   - plain pointers and sizes only; every function is callable from C and JNI;
  *   - int-returning functions return JL_OK (0) or a negative JL_ERR_* code and
  *     never throw; jl_last_error() gives a thread-local message;
- *   - "_dev" functions take device pointers (HBM) and an optional hipStream_t
- *     (void*; NULL = the engine's own stream) and are asynchronous unless noted;
+ *   - "_dev" functions take device pointers (HBM) and a hipStream_t (void*;
+ *     NULL = the HIP null stream) and are asynchronous unless noted;
  *     the other batch functions take host memory and block until done;
  *   - there is no CPU fallback behind the batch / verify entry points: with no
  *     usable GPU they fail with JL_ERR_NO_DEVICE.  Only the scalar Crc32C

@@ -79,7 +79,9 @@ int ensure_ready() {
     return r;
 }
 
-hipStream_t pick(void *stream) { return stream ? (hipStream_t)stream : ctx().stream; }
+// NULL is HIP's null (legacy default) stream, as everywhere in HIP, so device
+// entry points order with the caller's default-stream work.
+hipStream_t pick(void *stream) { return (hipStream_t)stream; }
 
 int grid_for(uint64_t blocks) {
     // one 1024-thread workgroup (16 waves) per CU; fewer when there is little work
@@ -180,12 +182,12 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
     if (block_bytes > 0xffffffffull) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: block_bytes >= 4 GiB");
     hipStream_t st = pick(stream);
     if (block_bytes == 4096) {
-        static const int nt = [] {
-            const char *e = getenv("JL_FIXED_NT");
-            return e ? atoi(e) : 1;
-        }();
+        // tuning knobs (A/B only; defaults are the measured best): JL_FIXED_NT, JL_FIXED_DEPTH
+        const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH");
+        const int nt = e_nt ? atoi(e_nt) : 1;
+        const int depth = e_d ? atoi(e_d) : 2;
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
-                                   grid_for(n_blocks), nt, st));
+                                   grid_for(n_blocks), nt, depth, st));
         return JL_OK;
     }
     jlk::KParams P = base_params(d_data, n_blocks, jlk::MODE_CRC);

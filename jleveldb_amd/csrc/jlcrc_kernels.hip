@@ -116,13 +116,14 @@ __device__ __forceinline__ void asm_load16(uint32_t w[16], const void *base, uin
 #undef JL_LD
 }
 
-// Chain over a block whose 16 loads were issued before the 16 loads of the next
-// block (and at most one store in between): word k is complete once at most
-// 31-k vector-memory operations are outstanding.
+// Chain over a block whose 16 loads were followed by the 16-load batches of D
+// later blocks (plus at most D stores): word k is complete once at most
+// 15-k + 16*D vector-memory operations are outstanding.
+template <int D>
 __device__ __forceinline__ uint32_t chain16_waited(uint32_t s, uint32_t w[16], const uint32_t *lds, uint32_t l4lo,
                                                    uint32_t l4hi) {
 #define JL_STEP(k)                                                                    \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[k]) : "n"(31 - k));                  \
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[k]) : "n"(15 - k + 16 * D));         \
     s = gstep(lds, s ^ w[k], l4lo, l4hi);
     JL_STEP(0) JL_STEP(1) JL_STEP(2) JL_STEP(3) JL_STEP(4) JL_STEP(5) JL_STEP(6) JL_STEP(7)
     JL_STEP(8) JL_STEP(9) JL_STEP(10) JL_STEP(11) JL_STEP(12) JL_STEP(13) JL_STEP(14) JL_STEP(15)
@@ -130,11 +131,15 @@ __device__ __forceinline__ uint32_t chain16_waited(uint32_t s, uint32_t w[16], c
     return s;
 }
 
-template <bool NT>
+// D = prefetch depth in blocks (1..3): while block b's chain runs, the loads of
+// blocks b+W .. b+D*W (W = waves in the grid) are in flight, i.e. up to
+// 16 waves x D x 4 KiB per CU.  Buffers rotate statically (loop unrolled D+1).
+template <bool NT, int D>
 __global__ __launch_bounds__(1024) void crc_fixed4k_kernel(const uint4 *__restrict__ img,
                                                            const uint8_t *__restrict__ data,
                                                            const uint8_t *__restrict__ zero, uint64_t n_blocks,
                                                            uint32_t flags, uint32_t *__restrict__ out) {
+    static_assert(D >= 1 && D <= 3, "vmcnt is 6 bits: at most 3 blocks ahead");
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u;
@@ -146,21 +151,25 @@ __global__ __launch_bounds__(1024) void crc_fixed4k_kernel(const uint4 *__restri
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t b = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     if (b >= n_blocks) return;
-    uint32_t wa[16], wb[16];
-    asm_load16<NT>(wa, data + b * 4096u, voff);
-    for (;;) {
-        uint64_t nb = b + waves;
-        asm_load16<NT>(wb, nb < n_blocks ? data + nb * 4096u : zero, voff);
-        uint32_t crc = ~wave_xor(realign(lds, chain16_waited(s_init, wa, lds, l4lo, l4hi), lc));
-        out[b] = do_mask ? mask_crc(crc) : crc;
-        if (nb >= n_blocks) break;
-        b = nb + waves;
-        asm_load16<NT>(wa, b < n_blocks ? data + b * 4096u : zero, voff);
-        crc = ~wave_xor(realign(lds, chain16_waited(s_init, wb, lds, l4lo, l4hi), lc));
-        out[nb] = do_mask ? mask_crc(crc) : crc;
-        if (b >= n_blocks) break;
+    uint32_t w[D + 1][16];
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+        const uint64_t bj = b + (uint64_t)j * waves;
+        asm_load16<NT>(w[j], bj < n_blocks ? data + bj * 4096u : zero, voff);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the final (zero-page) prefetch
+    for (;;) {
+#pragma unroll
+        for (int j = 0; j <= D; j++) {
+            const uint64_t bp = b + (uint64_t)D * waves;
+            asm_load16<NT>(w[(j + D) % (D + 1)], bp < n_blocks ? data + bp * 4096u : zero, voff);
+            const uint32_t crc = ~wave_xor(realign(lds, chain16_waited<D>(s_init, w[j], lds, l4lo, l4hi), lc));
+            out[b] = do_mask ? mask_crc(crc) : crc;
+            b += waves;
+            if (b >= n_blocks) goto done;
+        }
+    }
+done:
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
 }
 
 // ---------------------------------------------------------------------------
@@ -445,13 +454,20 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const v4u *__restrict_
 namespace jlk {
 
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
-                          uint32_t flags, uint32_t *out, int grid, int nt, hipStream_t st) {
-    if (nt)
-        hipLaunchKernelGGL(crc_fixed4k_kernel<true>, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, zero,
-                           n_blocks, flags, out);
-    else
-        hipLaunchKernelGGL(crc_fixed4k_kernel<false>, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, zero,
-                           n_blocks, flags, out);
+                          uint32_t flags, uint32_t *out, int grid, int nt, int depth, hipStream_t st) {
+#define JL_L(NTV, DV)                                                                                          \
+    hipLaunchKernelGGL((crc_fixed4k_kernel<NTV, DV>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, zero, \
+                       n_blocks, flags, out)
+    if (nt) {
+        if (depth <= 1) JL_L(true, 1);
+        else if (depth == 2) JL_L(true, 2);
+        else JL_L(true, 3);
+    } else {
+        if (depth <= 1) JL_L(false, 1);
+        else if (depth == 2) JL_L(false, 2);
+        else JL_L(false, 3);
+    }
+#undef JL_L
     return hipGetLastError();
 }
 

@@ -1,0 +1,33 @@
+package com.tchaicatkovsky.jleveldb.util;
+
+import java.nio.ByteBuffer;
+
+/**
+ * Static natives over libjlcrc.so (include/jlcrc.h) through jlcrc_jni.c.
+ * Loaded once; {@link #init(int)} binds the process to its GPU (the reference's
+ * Crc32C is static, so there is no per-instance state on the native side).
+ */
+public final class Crc32CNative {
+    static {
+        System.loadLibrary("jlcrc_jni");
+    }
+
+    private Crc32CNative() {}
+
+    public static native long value(byte[] data, int offset, int n);
+
+    public static native long extend(long initCrc, byte[] data, int offset, int n);
+
+    /** update() on the bit-flipped state held by a Crc32C instance. */
+    public static native int update(int state, byte[] data, int offset, int n);
+
+    public static native int init(int device);
+
+    public static native String lastError();
+
+    /** TableFormat.readBlock checksum test for many handles of one mmap'd table. */
+    public static native int tableVerify(ByteBuffer file, long[] offset, int[] size, byte[] status);
+
+    /** LogReader verification of a whole log image; returns the number of 16-byte events. */
+    public static native long logVerify(ByteBuffer log, boolean checksum, ByteBuffer events);
+}

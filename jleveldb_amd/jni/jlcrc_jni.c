@@ -1,0 +1,113 @@
+/*
+ * jlcrc_jni.c — JNI adapter from the reference's Java checksum surface to the
+ * C-ABI (include/jlcrc.h).  Built only where a JDK provides jni.h
+ * (`make -C jleveldb_amd/jni JAVA_HOME=...`); this image has no JDK.
+ *
+ * Java side: jleveldb_amd/jni/java/com/tchaicatkovsky/jleveldb/util/Crc32CNative.java
+ * (static natives) used by the patched Crc32C statics and by the batching shim
+ * at the four call sites, see INTEGRATION.md.
+ *
+ * Heap arrays are pinned with GetPrimitiveArrayCritical for the duration of the
+ * call (the C-ABI never retains pointers); direct ByteBuffers (mmap'd .ldb /
+ * .log regions) are passed zero-copy via GetDirectBufferAddress.
+ */
+#include <jni.h>
+#include <stdint.h>
+
+#include "../../include/jlcrc.h"
+
+#define JFN(name) Java_com_tchaicatkovsky_jleveldb_util_Crc32CNative_##name
+
+static void throw_(JNIEnv *env, const char *cls, const char *msg) {
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+static int range_ok(JNIEnv *env, jbyteArray a, jint off, jint n) {
+    jsize len = (*env)->GetArrayLength(env, a);
+    if (off < 0 || n < 0 || off > len - n) {
+        throw_(env, "java/lang/ArrayIndexOutOfBoundsException", "Crc32C range");
+        return 0;
+    }
+    return 1;
+}
+
+/* static long value(byte[] data, int offset, int n) — Crc32C.java:85-89 */
+JNIEXPORT jlong JNICALL JFN(value)(JNIEnv *env, jclass cls, jbyteArray data, jint off, jint n) {
+    (void)cls;
+    if (!range_ok(env, data, off, n)) return 0;
+    uint8_t *p = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
+    uint32_t v = jl_crc32c_value(p + off, (size_t)n);
+    (*env)->ReleasePrimitiveArrayCritical(env, data, p, JNI_ABORT);
+    return (jlong)v;
+}
+
+/* static long extend(long initCrc, byte[] data, int offset, int n) — Crc32C.java:43-48 */
+JNIEXPORT jlong JNICALL JFN(extend)(JNIEnv *env, jclass cls, jlong init, jbyteArray data, jint off, jint n) {
+    (void)cls;
+    if (!range_ok(env, data, off, n)) return 0;
+    uint8_t *p = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
+    uint32_t v = jl_crc32c_extend((uint32_t)init, p + off, (size_t)n);
+    (*env)->ReleasePrimitiveArrayCritical(env, data, p, JNI_ABORT);
+    return (jlong)v;
+}
+
+/* instance update(byte[],int,int) on the bit-flipped state — Crc32C.java:119-162 */
+JNIEXPORT jint JNICALL JFN(update)(JNIEnv *env, jclass cls, jint state, jbyteArray data, jint off, jint n) {
+    (void)cls;
+    if (!range_ok(env, data, off, n)) return state;
+    uint8_t *p = (*env)->GetPrimitiveArrayCritical(env, data, NULL);
+    uint32_t v = jl_crc32c_update((uint32_t)state, p + off, (size_t)n);
+    (*env)->ReleasePrimitiveArrayCritical(env, data, p, JNI_ABORT);
+    return (jint)v;
+}
+
+JNIEXPORT jint JNICALL JFN(init)(JNIEnv *env, jclass cls, jint device) {
+    (void)env; (void)cls;
+    return jl_init(device);
+}
+
+JNIEXPORT jstring JNICALL JFN(lastError)(JNIEnv *env, jclass cls) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, jl_last_error());
+}
+
+/* Batched TableFormat.readBlock checksum test over an mmap'd table (direct
+ * ByteBuffer): status[i] = 1 ok / 0 "block checksum mismatch". */
+JNIEXPORT jint JNICALL JFN(tableVerify)(JNIEnv *env, jclass cls, jobject file, jlongArray off, jintArray size,
+                                         jbyteArray status) {
+    (void)cls;
+    uint8_t *f = (*env)->GetDirectBufferAddress(env, file);
+    jlong cap = (*env)->GetDirectBufferCapacity(env, file);
+    jsize n = (*env)->GetArrayLength(env, off);
+    if (!f || cap < 0 || (*env)->GetArrayLength(env, size) != n || (*env)->GetArrayLength(env, status) != n) {
+        throw_(env, "java/lang/IllegalArgumentException", "tableVerify arguments");
+        return JL_ERR_INVALID;
+    }
+    jlong *o = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
+    jint *s = (*env)->GetPrimitiveArrayCritical(env, size, NULL);
+    jbyte *st = (*env)->GetPrimitiveArrayCritical(env, status, NULL);
+    int r = jl_table_verify(f, (uint64_t)cap, (const uint64_t *)o, (const uint32_t *)s, (uint64_t)n, (uint8_t *)st);
+    (*env)->ReleasePrimitiveArrayCritical(env, status, st, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, size, s, JNI_ABORT);
+    (*env)->ReleasePrimitiveArrayCritical(env, off, o, JNI_ABORT);
+    return r;
+}
+
+/* Batched LogReader verification of a whole .log / MANIFEST image (direct
+ * ByteBuffer): fills events as 16-byte jl_log_event records into `events`
+ * (a direct ByteBuffer); returns the event count or a negative error. */
+JNIEXPORT jlong JNICALL JFN(logVerify)(JNIEnv *env, jclass cls, jobject log, jboolean checksum, jobject events) {
+    (void)cls;
+    uint8_t *l = (*env)->GetDirectBufferAddress(env, log);
+    jlong bytes = (*env)->GetDirectBufferCapacity(env, log);
+    jl_log_event *ev = (*env)->GetDirectBufferAddress(env, events);
+    jlong evcap = (*env)->GetDirectBufferCapacity(env, events) / (jlong)sizeof(jl_log_event);
+    if (!l || !ev || bytes < 0 || evcap < 0) {
+        throw_(env, "java/lang/IllegalArgumentException", "logVerify arguments");
+        return JL_ERR_INVALID;
+    }
+    uint64_t n = 0;
+    int r = jl_log_verify(l, (uint64_t)bytes, checksum ? 1 : 0, ev, (uint64_t)evcap, &n);
+    return r ? (jlong)r : (jlong)n;
+}
