@@ -166,19 +166,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(args.steps):
+    ev[0].record(stream)
+    for i in range(args.steps):
         step()
-    e1.record(stream)
+        ev[i + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps
+    per_launch = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
+    kern_ms = sum(per_launch) / args.steps
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -218,6 +218,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "kernel_ms": round(kern_ms, 4),
+                "kernel_ms_min": round(min(per_launch), 4),
+                "kernel_ms_median": round(float(np.median(per_launch)), 4),
                 "alg_bytes_per_launch": alg_launch,
                 "read_stream_ceiling_GBps": round(ceiling, 1),
                 "frac_of_read_ceiling": round(achieved / ceiling, 4),

@@ -78,14 +78,20 @@ inline uint32_t unmask(uint32_t m) {
 // bytes:  G_j[i] = z^(252+j)(T0[i]), byte 0 of x uses G_3 ... byte 3 uses G_0.
 //
 // Region A (128 KiB): G_0..G_3 replicated 32x so that lane l always reads LDS
-//   bank (l & 31): dword index ((t*256 + i)*32 + b).  ds_read_b32 serves lanes
-//   0-31 and 32-63 in separate cycles, so 32 copies make every lookup
-//   conflict-free.
-// Region B (32 KiB): per-lane re-alignment tables.  After its last step lane l
-//   sits 4*l bytes past the end of the block, so its state is corrected with
-//   z^-(4*l), applied as 8 nibble lookups:  N_{l,j}[v] = z^-(4l)(v << 4j),
-//   dword index 32768 + (((l>>5)*8 + j)*16 + v)*32 + (l & 31).
+//   bank (l & 31) (ds_read_b32 serves lanes 0-31 and 32-63 in separate cycles,
+//   so 32 copies make every lookup conflict-free).  Table t, index i, copy b
+//   sits at byte address ((t>>1) << 16) | (i << 8) | ((t&1) << 7) | (b << 2):
+//   the index occupies exactly address byte 1, so the device builds each
+//   lookup address with one v_perm_b32 (byte k of x into byte 1, the lane's
+//   constant bytes 0 and 2 around it) — see gstep() in jlcrc_kernels.hip.
+// Region B (32 KiB, base 131072): per-lane re-alignment tables.  After its last
+//   step lane l sits 4*l bytes past the end of the block, so its state is
+//   corrected with z^-(4l), applied as 8 nibble lookups:
+//   N_{l,j}[v] = z^-(4l)(v << 4j), dword index 32768 + (((l>>5)*8 + j)*16 + v)*32 + (l & 31).
 // ----------------------------------------------------------------------------
+inline size_t g_dword_index(int t, int i, int b) {
+    return ((size_t)(t >> 1) << 14) | ((size_t)i << 6) | ((size_t)(t & 1) << 5) | (size_t)b;
+}
 constexpr int kGapBytes = 252;
 constexpr size_t kImageDwords = 32768 + 8192;
 constexpr size_t kImageBytes = kImageDwords * 4;  // 163840
@@ -96,7 +102,7 @@ inline std::vector<uint32_t> build_lds_image() {
     for (int t = 0; t < 4; t++)
         for (int i = 0; i < 256; i++) {
             uint32_t g = T.zn(T.t[0][i], (uint64_t)kGapBytes + t);
-            for (int b = 0; b < 32; b++) img[((size_t)t * 256 + i) * 32 + b] = g;
+            for (int b = 0; b < 32; b++) img[g_dword_index(t, i, b)] = g;
         }
     for (int l = 0; l < 64; l++)
         for (int j = 0; j < 8; j++)

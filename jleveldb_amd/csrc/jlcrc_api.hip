@@ -62,7 +62,8 @@ struct Context {
     hipStream_t stream = nullptr;
     void *d_img = nullptr;   // 160 KiB LDS image
     uint32_t *d_aux = nullptr;
-    uint8_t *d_zero = nullptr;  // 4 KiB of zeros
+    uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
+    uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
     // staging workspace (host-memory APIs, log verify)
     DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp;
 };
@@ -143,6 +144,7 @@ int jl_init(int device) {
     JL_HIP(hipMalloc(&c.d_img, jlmath::kImageBytes));
     JL_HIP(hipMalloc((void **)&c.d_aux, aux.size() * 4));
     JL_HIP(hipMalloc((void **)&c.d_zero, 4096));
+    JL_HIP(hipMalloc((void **)&c.d_scratch, 4096));
     JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     JL_HIP(hipMemcpy(c.d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice));
     JL_HIP(hipMemset(c.d_zero, 0, 4096));
@@ -163,6 +165,8 @@ int jl_shutdown(void) {
     (void)hipFree(c.d_img);
     (void)hipFree(c.d_aux);
     (void)hipFree(c.d_zero);
+    (void)hipFree(c.d_scratch);
+    c.d_scratch = nullptr;
     (void)hipStreamDestroy(c.stream);
     c.d_img = nullptr;
     c.d_aux = nullptr;
@@ -183,11 +187,12 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
     hipStream_t st = pick(stream);
     if (block_bytes == 4096) {
         // tuning knobs (A/B only; defaults are the measured best): JL_FIXED_NT, JL_FIXED_DEPTH
-        const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH");
+        const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH"), *e_c = getenv("JL_FIXED_CHAINS");
         const int nt = e_nt ? atoi(e_nt) : 1;
         const int depth = e_d ? atoi(e_d) : 2;
+        const int chains = e_c ? atoi(e_c) : 2;
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
-                                   grid_for(n_blocks), nt, depth, st));
+                                   ctx().d_scratch, grid_for(n_blocks), nt, depth, chains, st));
         return JL_OK;
     }
     jlk::KParams P = base_params(d_data, n_blocks, jlk::MODE_CRC);

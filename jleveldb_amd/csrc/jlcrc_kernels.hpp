@@ -43,7 +43,8 @@ struct LogEvent {  // layout-identical to jl_log_event
 };
 
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
-                          uint32_t flags, uint32_t *out, int grid, int nt, int depth, hipStream_t st);
+                          uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
+                          hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
 hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
                            const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st);

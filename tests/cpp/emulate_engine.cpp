@@ -29,8 +29,8 @@ static uint32_t emulate(const std::vector<uint32_t>& img, const uint8_t* base, u
             if (k == 0 && (uint32_t)lane == l0) s = inj;
             uint32_t x = s ^ w;
             uint32_t b = lane & 31;
-            s = img[((3 * 256) + (x & 0xff)) * 32 + b] ^ img[((2 * 256) + ((x >> 8) & 0xff)) * 32 + b] ^
-                img[((1 * 256) + ((x >> 16) & 0xff)) * 32 + b] ^ img[((0 * 256) + (x >> 24)) * 32 + b];
+            s = img[g_dword_index(3, x & 0xff, b)] ^ img[g_dword_index(2, (x >> 8) & 0xff, b)] ^
+                img[g_dword_index(1, (x >> 16) & 0xff, b)] ^ img[g_dword_index(0, x >> 24, b)];
         }
         uint32_t c = 0;
         for (int j = 0; j < 8; j++) {

@@ -21,19 +21,19 @@ data = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
 jl.fill_random_dev(data, 0x4A4C4442)
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 sink = torch.zeros(1, dtype=torch.int32, device="cuda")
-variants = [(nt, d) for nt in (1, 0) for d in (1, 2, 3)]
+variants = [(1, 1, 1), (1, 2, 1), (1, 3, 1), (1, 1, 2), (1, 1, 103), (1, 1, 104)]
 ref = None
 times = {v: [] for v in variants}
 times["read_stream"] = []
 for r in range(rounds):
     for v in variants:
-        os.environ["JL_FIXED_NT"], os.environ["JL_FIXED_DEPTH"] = str(v[0]), str(v[1])
+        os.environ["JL_FIXED_NT"], os.environ["JL_FIXED_DEPTH"], os.environ["JL_FIXED_CHAINS"] = map(str, v)
         jl.crc32c_fixed_dev(data, 4096, out=out)
         torch.cuda.synchronize()
         res = out.cpu().numpy()
         if ref is None:
             ref = res
-        assert np.array_equal(ref, res), v
+        assert v[2] > 100 or np.array_equal(ref, res), v
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
