@@ -27,9 +27,14 @@ def test_library_exports_every_declared_symbol(jl):
         assert hasattr(lib, s)
 
 
-def test_library_has_gfx950_code_object(jl):
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", jl.LIB_PATH],
-                         capture_output=True, text=True).stdout
+def test_library_has_gfx950_code_object(jl, tmp_path):
+    # llvm-objdump --offloading extracts the bundles next to its input: work on a copy
+    import shutil
+
+    lib_copy = tmp_path / "libjlcrc.so"
+    shutil.copy(jl.LIB_PATH, lib_copy)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib_copy)],
+                         capture_output=True, text=True, cwd=tmp_path).stdout
     assert "gfx950" in out
 
 
