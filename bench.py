@@ -10,7 +10,7 @@ C4 8M-block set, generated in place (weak scaling, no data-path collective);
 value = all ranks' bytes / max-over-ranks time.
 
 Also reported on the same JSON line:
-  roofline     — dominant kernel (crc_fixed4k_kernel) timed with HIP events on
+  roofline     — dominant kernel (crc_fixed4k_x2_kernel) timed with HIP events on
                  its launch stream; algorithmic bytes = 4096 B read + 4 B
                  written per block; peak = 8.0 TB/s (MI355X spec);
                  measured read-stream ceiling beside it; traffic from the
@@ -210,7 +210,7 @@ def main():
                        "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "crc_fixed4k_kernel",
+                "kernel": "crc_fixed4k_x2_kernel<nt, bitop3>",
                 "achieved": round(achieved, 1),
                 "peak": PEAK_GBS,
                 "unit": "GB/s",

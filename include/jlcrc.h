@@ -74,6 +74,15 @@ const char *jl_version(void);
 int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags,
                         uint32_t *d_out, void *stream);
 
+/* Host-memory form of jl_crc32c_fixed_dev for blocks that start in host memory
+ * (an mmap'd file, a pinned buffer): streams them through the engine in chunks
+ * (JL_STREAM_CHUNK_BYTES), two HIP streams alternating so the H2D copy of
+ * chunk i+1 overlaps the kernel of chunk i; out[] (host) is filled on return.
+ * Pinned / hipHostRegister'ed memory is DMA'd directly; pageable memory is
+ * first copied into pinned staging buffers.  Bound by PCIe, not HBM. */
+int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags, uint32_t *out);
+#define JL_STREAM_CHUNK_BYTES (64ull << 20)
+
 /* Arbitrary blocks in one arena: block i = d_base[d_off[i], d_off[i]+d_len[i]).
  * d_init (nullable): per-block initial crc as in Crc32C.extend(init, ...),
  *   J/util/Crc32C.java:43-48 (LogWriter uses typeCrc[t], J/db/LogWriter.java:147).

@@ -79,6 +79,7 @@ def lib() -> ctypes.CDLL:
         "jl_version": (ctypes.c_char_p, []),
         "jl_crc32c_fixed_dev": (i32, [vp, u64, u64, u32, vp, vp]),
         "jl_crc32c_batch_dev": (i32, [vp, vp, vp, vp, vp, u64, u32, vp, vp]),
+        "jl_crc32c_fixed": (i32, [vp, u64, u64, u32, vp]),
         "jl_crc32c_batch": (i32, [vp, u64, vp, vp, vp, vp, u64, u32, vp]),
         "jl_table_trailers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
         "jl_table_verify_dev": (i32, [vp, vp, vp, u64, vp, vp]),
@@ -221,6 +222,23 @@ def crc32c_fixed_dev(data, block_bytes: int, n_blocks: int | None = None, flags:
         out = torch.empty(n_blocks, dtype=torch.int32, device=data.device)
     _check(lib().jl_crc32c_fixed_dev(_dptr(data), block_bytes, n_blocks, flags, _dptr(out), _stream(stream)),
            "jl_crc32c_fixed_dev")
+    return out
+
+
+def crc32c_fixed(data, block_bytes: int, n_blocks: int | None = None, flags: int = FLAG_MASK) -> np.ndarray:
+    """Host-memory blocks (numpy array, bytes, or a pinned CPU tensor), streamed
+    through the engine with overlapped H2D copies (jl_crc32c_fixed)."""
+    if hasattr(data, "data_ptr"):  # torch CPU tensor (pinned or not)
+        ptr, nbytes = data.data_ptr(), data.numel() * data.element_size()
+    else:
+        a = _host(data)
+        ptr, nbytes = a.ctypes.data, a.size
+    if n_blocks is None:
+        n_blocks = nbytes // block_bytes
+    if n_blocks * block_bytes > nbytes:
+        raise JLError("crc32c_fixed: buffer smaller than n_blocks * block_bytes")
+    out = np.zeros(n_blocks, dtype=np.uint32)
+    _check(lib().jl_crc32c_fixed(ptr, block_bytes, n_blocks, flags, out.ctypes.data), "jl_crc32c_fixed")
     return out
 
 

@@ -66,6 +66,15 @@ struct Context {
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
     // staging workspace (host-memory APIs, log verify)
     DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp;
+    // streaming pipeline (jl_crc32c_fixed): two slots, each a device chunk + result
+    // buffer, a pinned staging buffer (pageable sources) and its own stream
+    struct Slot {
+        DevBuf d_in, d_out;
+        void *h_stage = nullptr;
+        size_t h_cap = 0;
+        hipStream_t st = nullptr;
+        hipEvent_t done = nullptr;
+    } slot[2];
 };
 
 Context &ctx() {
@@ -162,6 +171,14 @@ int jl_shutdown(void) {
     for (DevBuf *b : {&c.ws_data, &c.ws_off, &c.ws_len, &c.ws_init, &c.ws_sfx, &c.ws_out, &c.ws_cnt, &c.ws_start,
                       &c.ws_ev, &c.ws_ok, &c.ws_tmp})
         b->release();
+    for (auto &sl : c.slot) {
+        sl.d_in.release();
+        sl.d_out.release();
+        if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+        if (sl.done) (void)hipEventDestroy(sl.done);
+        if (sl.st) (void)hipStreamDestroy(sl.st);
+        sl = Context::Slot();
+    }
     (void)hipFree(c.d_img);
     (void)hipFree(c.d_aux);
     (void)hipFree(c.d_zero);
@@ -190,7 +207,7 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
         const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH"), *e_c = getenv("JL_FIXED_CHAINS");
         const int nt = e_nt ? atoi(e_nt) : 1;
         const int depth = e_d ? atoi(e_d) : 2;
-        const int chains = e_c ? atoi(e_c) : 2;
+        const int chains = e_c ? atoi(e_c) : 3;
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
                                    ctx().d_scratch, grid_for(n_blocks), nt, depth, chains, st));
         return JL_OK;
@@ -200,6 +217,51 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
     P.flags = flags;
     P.out32 = d_out;
     return run_general(P, st);
+}
+
+int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags, uint32_t *out) {
+    if (int r = ensure_ready()) return r;
+    if (n_blocks == 0) return JL_OK;
+    if (!host || !out || block_bytes == 0) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: bad arguments");
+    if (block_bytes > JL_STREAM_CHUNK_BYTES) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: block larger than a chunk");
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    hipPointerAttribute_t attr;
+    bool pinned = hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // pageable memory reports an error here; clear it
+    const uint64_t per = JL_STREAM_CHUNK_BYTES / block_bytes;  // blocks per chunk
+    const uint64_t chunk_bytes = per * block_bytes;
+    for (auto &sl : c.slot) {
+        if (!sl.st) JL_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+        if (!sl.done) JL_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+        JL_HIP(sl.d_in.ensure(chunk_bytes));
+        JL_HIP(sl.d_out.ensure(per * 4));
+        if (!pinned && sl.h_cap < chunk_bytes) {
+            if (sl.h_stage) (void)hipHostFree(sl.h_stage);
+            sl.h_stage = nullptr;
+            sl.h_cap = 0;
+            if (hipHostMalloc(&sl.h_stage, chunk_bytes, hipHostMallocDefault) != hipSuccess)
+                return fail(JL_ERR_NOMEM, "jl_crc32c_fixed: pinned staging allocation failed");
+            sl.h_cap = chunk_bytes;
+        }
+    }
+    for (uint64_t b0 = 0, i = 0; b0 < n_blocks; b0 += per, i++) {
+        Context::Slot &sl = c.slot[i & 1];
+        const uint64_t nb = std::min(per, n_blocks - b0);
+        const uint8_t *src = host + b0 * block_bytes;
+        if (!pinned) {  // the slot's previous copy out of its staging buffer must be done
+            JL_HIP(hipEventSynchronize(sl.done));
+            memcpy(sl.h_stage, src, nb * block_bytes);
+            src = (const uint8_t *)sl.h_stage;
+        }
+        JL_HIP(hipMemcpyAsync(sl.d_in.p, src, nb * block_bytes, hipMemcpyHostToDevice, sl.st));
+        if (int r = jl_crc32c_fixed_dev(sl.d_in.p, block_bytes, nb, flags, (uint32_t *)sl.d_out.p, sl.st)) return r;
+        JL_HIP(hipMemcpyAsync(out + b0, sl.d_out.p, nb * 4, hipMemcpyDeviceToHost, sl.st));
+        JL_HIP(hipEventRecord(sl.done, sl.st));
+    }
+    JL_HIP(hipStreamSynchronize(c.slot[0].st));
+    JL_HIP(hipStreamSynchronize(c.slot[1].st));
+    return JL_OK;
 }
 
 int jl_crc32c_batch_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint32_t *d_init,

@@ -249,7 +249,43 @@ __device__ __forceinline__ void chain_pair(uint32_t &sa, uint32_t &sb, uint32_t 
 #undef JL_STEP2
 }
 
-template <bool NT>
+// 3-input XOR in one issue slot: gfx950's v_bitop3_b32 with truth table 0x96
+// (the compiler does not form it on its own from a ^ b ^ c).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Four G lookups of x, XOR-folded together with `w` (the next step's data word
+// or 0): 4 v_perm_b32 + 4 ds_read_b32 + 2 v_bitop3_b32 per step instead of
+// 1 + 4 + 3 separate XORs.
+__device__ __forceinline__ uint32_t gstep_x3(const uint32_t *lds, uint32_t x, const GLanes &g, uint32_t w) {
+    uint32_t v0 = lds_at(lds, JL_GADDR(g.l3, x, 0u));
+    uint32_t v1 = lds_at(lds, JL_GADDR(g.l2, x, 1u));
+    uint32_t v2 = lds_at(lds, JL_GADDR(g.l1, x, 2u));
+    uint32_t v3 = lds_at(lds, JL_GADDR(g.l0, x, 3u));
+    return xor3(xor3(v0, v1, v2), v3, w);
+}
+
+// chain_pair with the data XOR folded into the previous step's xor3: on entry
+// the states are the raw chain states (s_init); a[k]/b[k] wait as in chain_pair.
+__device__ __forceinline__ void chain_pair_x3(uint32_t &sa, uint32_t &sb, uint32_t a[16], uint32_t b[16],
+                                              const uint32_t *lds, const GLanes &gl) {
+    asm volatile("s_waitcnt vmcnt(63)" : "+v"(a[0]));
+    asm volatile("s_waitcnt vmcnt(62)" : "+v"(b[0]));
+    uint32_t xa = sa ^ a[0], xb = sb ^ b[0];
+#define JL_STEP3(k)                                                               \
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a[k]) : "n"(63 - 2 * k));           \
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(b[k]) : "n"(62 - 2 * k));           \
+    xa = gstep_x3(lds, xa, gl, a[k]);                                             \
+    xb = gstep_x3(lds, xb, gl, b[k]);
+    JL_STEP3(1) JL_STEP3(2) JL_STEP3(3) JL_STEP3(4) JL_STEP3(5) JL_STEP3(6) JL_STEP3(7) JL_STEP3(8)
+    JL_STEP3(9) JL_STEP3(10) JL_STEP3(11) JL_STEP3(12) JL_STEP3(13) JL_STEP3(14) JL_STEP3(15)
+#undef JL_STEP3
+    sa = gstep_x3(lds, xa, gl, 0u);
+    sb = gstep_x3(lds, xb, gl, 0u);
+}
+
+template <bool NT, bool X3 = false, bool PRIO = false>
 __global__ __launch_bounds__(1024) void crc_fixed4k_x2_kernel(const uint4 *__restrict__ img,
                                                               const uint8_t *__restrict__ data,
                                                               const uint8_t *__restrict__ zero, uint64_t n_blocks,
@@ -281,10 +317,13 @@ __global__ __launch_bounds__(1024) void crc_fixed4k_x2_kernel(const uint4 *__res
     for (;;) {
 #define JL_PAIR(CA, CB, NA, NB)                                                                          \
     {                                                                                                    \
+        if (PRIO) __builtin_amdgcn_s_setprio(3);                                                          \
         asm_load32x2<NT>(NA, NB, src(pg * 64u + pj), src(pg * 64u + pj + 1), voff);                      \
+        if (PRIO) __builtin_amdgcn_s_setprio(0);                                                          \
         adv(pg, pj);                                                                                     \
         uint32_t sa = s_init, sb = s_init;                                                               \
-        chain_pair(sa, sb, CA, CB, lds, gl);                                                             \
+        if (X3) chain_pair_x3(sa, sb, CA, CB, lds, gl);                                                  \
+        else chain_pair(sa, sb, CA, CB, lds, gl);                                                        \
         uint32_t ca = ~wave_xor(realign(lds, sa, lc)), cb = ~wave_xor(realign(lds, sb, lc));             \
         if (do_mask) { ca = mask_crc(ca); cb = mask_crc(cb); }                                           \
         res = (lane == (uint32_t)j) ? ca : res;                                                          \
@@ -658,23 +697,38 @@ __global__ void fill_random_tail_kernel(uint8_t *__restrict__ dst, uint64_t byte
     for (uint64_t i = w * 8, j = 0; i < bytes; i++, j++) dst[i] = (uint8_t)(z >> (8 * j));
 }
 
-// Read-only HBM stream (calibration for the roofline): every workgroup XOR-folds
-// its grid-stride share of the buffer with 16-B loads and writes one word.
+// Read-only HBM stream (calibration for the roofline).  The fastest read shape
+// measured on MI355X (tools/hbm_probe.hip, profiles/r1b_hbm_probe.log): LDS-DMA
+// (global_load_lds_dwordx4 ... nt), each wave streaming 8 KiB pieces into its
+// own 8 x 1 KiB LDS ring, 4 waves per workgroup, 8 workgroups per CU.  Bytes
+// past the last whole 8 KiB piece are read with plain 16-B loads.
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void read_stream_kernel(const v4u *__restrict__ src, uint64_t n16,
+__global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t *__restrict__ src, uint64_t bytes,
                                                           uint32_t *__restrict__ sink) {
-    v4u acc = {0, 0, 0, 0};
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        v4u a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride);
-        v4u c = __builtin_nontemporal_load(src + i + 2 * stride), d = __builtin_nontemporal_load(src + i + 3 * stride);
-        acc ^= a ^ b ^ c ^ d;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[4][8][1024];
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t waves = (uint64_t)gridDim.x * 4u;
+    const uint64_t pieces = bytes / 8192u;
+    uint32_t acc = 0;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4u + wv; c < pieces; c += waves) {
+        const uint8_t *p = src + c * 8192u + lane * 16u;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            __builtin_amdgcn_global_load_lds((const void *)(p + k * 1024), (__attribute__((address_space(3))) void *)&ring[wv][k][0],
+                                             16, 0, 2 /* nt */);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        acc ^= *(const uint32_t *)&ring[wv][lane & 7u][(lane >> 3) * 4u];
     }
-    for (; i < n16; i += stride) acc ^= src[i];
-    uint32_t v = wave_xor(acc.x ^ acc.y ^ acc.z ^ acc.w);
-    if ((threadIdx.x & 63u) == 0) atomicXor(sink, v);
+    const uint64_t t0 = pieces * 8192u / 16u, n16 = bytes / 16u;
+    for (uint64_t i = t0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+        v4u v = ((const v4u *)src)[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    // one conditional store per wave (the loads must not be dead code): 8k
+    // same-address atomics at the end of the grid cost ~75 us (r1 measurement)
+    acc = wave_xor(acc);
+    if (lane == 0 && acc == 0x6a4c4442u) *sink = acc;
 }
 
 }  // namespace jlk
@@ -685,6 +739,21 @@ namespace jlk {
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st) {
+    if (chains == 3) {  // two chains + bitop3 XOR folding (default)
+        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img,
+                           data, zero, n_blocks, flags, out);
+        return hipGetLastError();
+    }
+    if (chains == 4) {  // A/B: + s_setprio 3 around the load issue
+        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true, true>), dim3(grid), dim3(1024), 0, st,
+                           (const uint4 *)img, data, zero, n_blocks, flags, out);
+        return hipGetLastError();
+    }
+    if (chains == 5 || chains == 6) {  // A/B: 8 / 12 waves per CU
+        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true>), dim3(grid), dim3(chains == 5 ? 512 : 768), 0, st,
+                           (const uint4 *)img, data, zero, n_blocks, flags, out);
+        return hipGetLastError();
+    }
     if (chains == 2) {
         if (nt)
             hipLaunchKernelGGL(crc_fixed4k_x2_kernel<true>, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data,
@@ -742,7 +811,7 @@ hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const 
 }
 
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(256), 0, st, (const v4u *)src, bytes / 16, sink);
+    hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, bytes, sink);
     return hipGetLastError();
 }
 

@@ -295,3 +295,26 @@ def test_full_size_c2_block_for_block(gpu, jl, oracle):
     got2 = u32(jl.crc32c_fixed_dev(data, 4096))
     diff = np.nonzero(got2 != got)[0]
     assert list(diff) == [123456]
+
+
+# ------------------------------------------------- host-memory streaming path
+@pytest.mark.parametrize("block_bytes,n_blocks", [(4096, 2 * 16384 + 100), (1000, 70000), (4096, 3), (65536, 1025)])
+def test_fixed_host_streaming_pageable(gpu, jl, oracle, block_bytes, n_blocks):
+    """jl_crc32c_fixed over pageable host memory: several 64 MiB chunks + a partial one."""
+    rng = np.random.default_rng(block_bytes + n_blocks)
+    host = rng.integers(0, 256, block_bytes * n_blocks, dtype=np.uint8)
+    got = jl.crc32c_fixed(host, block_bytes)
+    assert np.array_equal(got, oracle.fixed(host, block_bytes, n_blocks, threads=THREADS))
+    raw = jl.crc32c_fixed(host, block_bytes, flags=0)
+    assert np.array_equal(raw, oracle.fixed(host, block_bytes, n_blocks, flags=0, threads=THREADS))
+
+
+def test_fixed_host_streaming_pinned(gpu, jl, oracle):
+    import torch
+
+    n = 16384 + 77
+    t = torch.empty(n * 4096, dtype=torch.uint8, pin_memory=True)
+    rng = np.random.default_rng(5)
+    t.numpy()[:] = rng.integers(0, 256, n * 4096, dtype=np.uint8)
+    got = jl.crc32c_fixed(t, 4096)
+    assert np.array_equal(got, oracle.fixed(t.numpy(), 4096, n, threads=THREADS))

@@ -120,13 +120,25 @@ __global__ __launch_bounds__(256) void rd_ldsdma(const uint8_t *__restrict__ s, 
     if (acc == 0x12345678u) atomicAdd(sink, 1u);
 }
 
+__global__ void fill_rand(uint64_t *d, uint64_t words) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = 0x4A4C4442ull + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        d[i] = z ^ (z >> 31);
+    }
+}
+
 int main(int argc, char **argv) {
     size_t bytes = (size_t)4 << 30;
     uint8_t *d;
     uint32_t *sink;
     CK(hipMalloc(&d, bytes));
     CK(hipMalloc(&sink, 4));
-    CK(hipMemset(d, 0x5a, bytes));
+    // random bytes: HBM read rates measured on constant data are higher than on
+    // real data (profiles/r1b_*), so the probe reads what the engine reads
+    fill_rand<<<4096, 256>>>((uint64_t *)d, bytes / 8);
+    CK(hipDeviceSynchronize());
     hipDeviceProp_t p;
     CK(hipGetDeviceProperties(&p, 0));
     int cu = p.multiProcessorCount;
@@ -144,7 +156,7 @@ int main(int argc, char **argv) {
         {"chunk2_lds_pf", 13, cu},
         {"ldsdma_nt_g1024", 8, cu * 4}, {"ldsdma_plain_g1024", 9, cu * 4}, {"ldsdma_nt_g2048", 8, cu * 8},
     };
-    const int rounds = 5, reps = 5;
+    const int rounds = argc > 1 ? atoi(argv[1]) : 5, reps = argc > 2 ? atoi(argv[2]) : 5;
     std::vector<std::vector<float>> t(vs.size());
     for (int r = 0; r < rounds; r++)
         for (size_t v = 0; v < vs.size(); v++) {

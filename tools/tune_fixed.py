@@ -21,7 +21,7 @@ data = torch.empty(n * 4096, dtype=torch.uint8, device="cuda")
 jl.fill_random_dev(data, 0x4A4C4442)
 out = torch.empty(n, dtype=torch.int32, device="cuda")
 sink = torch.zeros(1, dtype=torch.int32, device="cuda")
-variants = [(1, 1, 1), (1, 2, 1), (1, 3, 1), (1, 1, 2), (1, 1, 103), (1, 1, 104)]
+variants = [tuple(int(x) for x in v.split(",")) for v in os.environ.get("VARIANTS", "1,1,2 1,1,3 1,1,103").split()]
 ref = None
 times = {v: [] for v in variants}
 times["read_stream"] = []
