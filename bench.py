@@ -130,6 +130,73 @@ def secondary_c3(dev, stream, steps, warmup):
     return res
 
 
+def secondary_c5(dev, stream, steps, warmup):
+    """Config C5: streaming WAL verification over 2^17 x 32 KiB log blocks (4 GiB).
+
+    The log is produced on the device by the product's batched LogWriter
+    (jl_log_layout + jl_log_emit_dev) from C1-shaped records (1 056-B payload =
+    12-B batch header + 16-B key + 1 KiB value varints included), then verified
+    with jl_log_verify_dev (header walk + per-record masked-CRC check with
+    LogReader.readPhysicalRecord semantics).  Timed device-resident, and
+    copy-inclusive from pinned host memory through jl_log_verify."""
+    rec = 1056
+    target = (1 << 17) * 32768
+    n_rec = target // (rec + 7)
+    lens = np.full(n_rec, rec, np.uint32)
+    offs = np.arange(n_rec, dtype=np.uint64) * rec
+    plan = jl.log_layout(offs, lens)
+    src = torch.empty(n_rec * rec, dtype=torch.uint8, device=dev)
+    jl.fill_random_dev(src, SEED + 5)
+    log = jl.log_emit_dev(src, plan)
+    del src
+    nb = plan["log_bytes"]
+    crc_bytes = int(plan["len"].sum(dtype=np.uint64)) + plan["len"].size  # type byte || payload
+    events = torch.empty((nb // 7 + 2) * 16, dtype=torch.uint8, device=dev)
+    fn = lambda: jl.log_verify_dev(log, events=events)  # noqa: E731
+    ev, n_ev = fn()
+    kinds = ev[: n_ev * 16].view(-1, 16)[:, 13].cpu().numpy()
+    ok = int((kinds == jl.LOG_OK).sum())
+    wall, ms = timed(fn, steps, warmup, stream)
+    res = {"config": "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident",
+           "log_bytes": nb, "records": int(plan["len"].size), "records_ok": ok,
+           "GiB_per_s": round(nb / (wall / steps) / GIB, 1),
+           "achieved_GBps": round((crc_bytes + 7 * plan["len"].size) / (wall / steps) / 1e9, 1),
+           "ms_per_step": round(wall / steps * 1e3, 3)}
+    host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    host.copy_(log)
+    del log, events
+    torch.cuda.empty_cache()
+    hn = host.numpy()
+    jl.log_verify(hn)
+    t0 = time.perf_counter()
+    hev = jl.log_verify(hn)
+    el = time.perf_counter() - t0
+    res["copy_inclusive_GiB_per_s"] = round(nb / el / GIB, 2)
+    res["copy_inclusive_records_ok"] = int((hev["kind"] == jl.LOG_OK).sum())
+    return res
+
+
+def copy_inclusive_c2(data):
+    """C2 bytes starting in host memory: jl_crc32c_fixed (H2D overlapped with the
+    kernel on two streams), pinned and pageable sources."""
+    nbytes = data.numel()
+    pinned = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(data)
+    ref = jl.crc32c_fixed(pinned, 4096)
+    t0 = time.perf_counter()
+    jl.crc32c_fixed(pinned, 4096)
+    pin_s = time.perf_counter() - t0
+    pageable = pinned.numpy().copy()
+    del pinned
+    jl.crc32c_fixed(pageable[: 64 << 20], 4096)
+    t0 = time.perf_counter()
+    got = jl.crc32c_fixed(pageable, 4096)
+    page_s = time.perf_counter() - t0
+    return {"config": "C2 from host memory (H2D + kernel + D2H, 64 MiB chunks, 2 streams)",
+            "pinned_GiB_per_s": round(nbytes / pin_s / GIB, 2), "pageable_GiB_per_s": round(nbytes / page_s / GIB, 2),
+            "parity_with_device_resident": bool(np.array_equal(ref, got))}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,9 +295,14 @@ def main():
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(data, n, gpu_out, args.cpu_seconds)
     if world == 1 and not args.no_secondary:
+        sec = [copy_inclusive_c2(data)]
+        sec[0]["parity_with_device_resident"] &= bool(np.array_equal(gpu_out, out.cpu().numpy().view(np.uint32)))
         del data
         torch.cuda.empty_cache()
-        result["secondary"] = [secondary_c3(dev, stream, 5, 2)]
+        sec.append(secondary_c3(dev, stream, 5, 2))
+        torch.cuda.empty_cache()
+        sec.append(secondary_c5(dev, stream, 5, 2))
+        result["secondary"] = sec
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

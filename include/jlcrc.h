@@ -184,6 +184,27 @@ int jl_log_read_records(const uint8_t *log, uint64_t log_bytes, int checksum, ui
 int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint8_t *d_type,
                        uint64_t n, uint8_t *d_header, void *stream);
 
+/* Framing plan of LogWriter.addRecord (J/db/LogWriter.java:88-134) for n
+ * records appended to a log that is dest_length bytes long (LogWriter(dest,
+ * destLength), :80-84): record r is src[rec_src_off[r], +rec_len[r]).  For every
+ * physical fragment f: frag_hdr_off[f] = offset of its 7-byte header in the
+ * appended bytes, frag_src_off[f] = its payload's offset in src, frag_len[f],
+ * frag_type[f] (Full/First/Middle/Last).  Bytes not covered by a fragment are
+ * the zero-filled block trailers (:101-107).  *n_frags / *log_bytes get the
+ * totals; JL_ERR_CAPACITY when cap < *n_frags.  Host only, no checksum work. */
+int jl_log_layout(const uint64_t *rec_src_off, const uint32_t *rec_len, uint64_t n, uint64_t dest_length,
+                  uint64_t *frag_hdr_off, uint64_t *frag_src_off, uint32_t *frag_len, uint8_t *frag_type,
+                  uint64_t cap, uint64_t *n_frags, uint64_t *log_bytes);
+
+/* Batched LogWriter on the device: writes the log_bytes appended bytes of a
+ * jl_log_layout plan to d_log — zero trailers, payload copied from d_src, and
+ * every header [LE32 mask(extend(typeCrc[t], payload))][LE16 len][type]
+ * (emitPhysicalRecord, J/db/LogWriter.java:136-161).  Asynchronous on stream;
+ * the plan arrays are device pointers. */
+int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uint64_t *d_frag_src_off,
+                    const uint32_t *d_frag_len, const uint8_t *d_frag_type, uint64_t n_frags, uint64_t log_bytes,
+                    uint8_t *d_log, void *stream);
+
 /* ------------------------------------------------------------ bench helpers */
 /* Fills d_dst[0, bytes) with the splitmix64 stream used by the benches
  * (word i = splitmix64(seed + (first_word + i + 1) * golden)), on device. */

@@ -53,7 +53,7 @@ def build(force: bool = False) -> str:
     import subprocess
 
     if force or not os.path.exists(LIB_PATH):
-        subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc"), "-j4"], check=True)
+        subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc"), "-j8"], check=True)
     return LIB_PATH
 
 
@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
         "jl_log_read_records": (i32, [vp, u64, i32, u64, vp, u64, vp, u64, ctypes.POINTER(u64), vp, u64,
                                       ctypes.POINTER(u64)]),
         "jl_log_headers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
+        "jl_log_layout": (i32, [vp, vp, u64, u64, vp, vp, vp, vp, u64, vp, vp]),
+        "jl_log_emit_dev": (i32, [vp, vp, vp, vp, vp, u64, u64, vp, vp]),
         "jl_fill_random_dev": (i32, [vp, u64, u64, u64, vp]),
         "jl_read_stream_dev": (i32, [vp, u64, vp, vp]),
     }
@@ -311,6 +313,44 @@ def log_headers_dev(base, off, length, types, out=None, stream=None):
     _check(lib().jl_log_headers_dev(_dptr(base), _dptr(off), _dptr(length), _dptr(types), n, _dptr(out),
                                     _stream(stream)), "jl_log_headers_dev")
     return out
+
+
+def log_layout(rec_src_off, rec_len, dest_length: int = 0):
+    """LogWriter.addRecord framing plan (jl_log_layout): dict of numpy arrays
+    hdr_off / src_off / len / type per physical fragment, plus log_bytes."""
+    so = np.ascontiguousarray(rec_src_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(rec_len, dtype=np.uint32)
+    n = ln.size
+    # a record of L bytes spans at most L // 32761 + 2 fragments
+    cap = int((ln.astype(np.uint64) // 32761).sum()) + 2 * n + 1
+    hdr = np.zeros(cap, np.uint64)
+    src = np.zeros(cap, np.uint64)
+    fl = np.zeros(cap, np.uint32)
+    ft = np.zeros(cap, np.uint8)
+    nf, lb = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(lib().jl_log_layout(so.ctypes.data, ln.ctypes.data, n, dest_length, hdr.ctypes.data, src.ctypes.data,
+                               fl.ctypes.data, ft.ctypes.data, cap, ctypes.byref(nf), ctypes.byref(lb)),
+           "jl_log_layout")
+    k = nf.value
+    return {"hdr_off": hdr[:k], "src_off": src[:k], "len": fl[:k], "type": ft[:k], "log_bytes": lb.value}
+
+
+def log_emit_dev(src, plan, out=None, stream=None):
+    """Batched LogWriter on the device (jl_log_emit_dev): the log image (uint8
+    tensor) of a log_layout plan over the device arena `src`."""
+    import torch
+
+    dev = src.device
+    t = {k: torch.from_numpy(np.ascontiguousarray(plan[k]).view(
+        {"hdr_off": np.int64, "src_off": np.int64, "len": np.int32, "type": np.uint8}[k])).to(dev)
+        for k in ("hdr_off", "src_off", "len", "type")}
+    nb = plan["log_bytes"]
+    if out is None:
+        out = torch.empty(max(nb, 1), dtype=torch.uint8, device=dev)
+    _check(lib().jl_log_emit_dev(_dptr(src), _dptr(t["hdr_off"]), _dptr(t["src_off"]), _dptr(t["len"]),
+                                 _dptr(t["type"]), plan["len"].size, nb, _dptr(out), _stream(stream)),
+           "jl_log_emit_dev")
+    return out[:nb]
 
 
 def log_verify(log, checksum: bool = True) -> np.ndarray:

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
+#include <utility>
 #include <vector>
 
 namespace jlmath {
@@ -113,11 +114,49 @@ inline std::vector<uint32_t> build_lds_image() {
     return img;
 }
 
+// slice4(x) = state after feeding the 4 LE bytes of x to a zero state
+// (T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]); linear and invertible over GF(2).
+inline uint32_t slice4(uint32_t x) {
+    const Tables &T = tables();
+    return T.t[3][x & 0xffu] ^ T.t[2][(x >> 8) & 0xffu] ^ T.t[1][(x >> 16) & 0xffu] ^ T.t[0][x >> 24];
+}
+// Seed word of the stream kernel: feeding W = slice4^-1(~init) as the 4 data
+// bytes just before a block turns a zero state into ~init at the block start,
+// so `extend(init, ...)` needs no state shift.
+inline uint32_t slice4_inv(uint32_t y) {
+    static const std::vector<uint32_t> cols = [] {  // columns of slice4^-1 by Gauss-Jordan
+        uint32_t a[32], inv[32];
+        for (int i = 0; i < 32; i++) {
+            a[i] = slice4(1u << i);  // column i of the forward map
+            inv[i] = 1u << i;
+        }
+        // row-reduce the set of (image, preimage) pairs so image i == bit i
+        for (int bit = 0; bit < 32; bit++) {
+            int piv = -1;
+            for (int i = bit; i < 32; i++)
+                if ((a[i] >> bit) & 1u) { piv = i; break; }
+            if (piv < 0) throw std::logic_error("slice4 is not invertible");
+            std::swap(a[piv], a[bit]);
+            std::swap(inv[piv], inv[bit]);
+            for (int i = 0; i < 32; i++)
+                if (i != bit && ((a[i] >> bit) & 1u)) { a[i] ^= a[bit]; inv[i] ^= inv[bit]; }
+        }
+        return std::vector<uint32_t>(inv, inv + 32);  // slice4(inv[i]) == 1 << i
+    }();
+    uint32_t x = 0;
+    for (int i = 0; i < 32; i++)
+        if ((y >> i) & 1u) x ^= cols[i];
+    return x;
+}
+
 // Small global-memory table used by the kernels' scalar epilogues:
-//   [0,256)   T0
-//   [256,512) inv_top (as u32)
-//   [512,517) typeCrc[0..4] = value([t])  (LogWriter.initTypeCrc, J/db/LogWriter.java:51-57)
-constexpr size_t kAuxDwords = 520;
+//   [0,256)     T0
+//   [256,512)   inv_top (as u32)
+//   [512,517)   typeCrc[0..4] = value([t])  (LogWriter.initTypeCrc, J/db/LogWriter.java:51-57)
+//   [520,525)   W(typeCrc[t]) = slice4^-1(~typeCrc[t])   (stream-kernel seeds)
+//   [525]       W(0) = slice4^-1(0xffffffff)               (value(): init 0)
+//   [528,1552)  U_j[v] = slice4^-1(v << 8j), j = 0..3     (seed of an arbitrary init)
+constexpr size_t kAuxDwords = 1552;
 inline std::vector<uint32_t> build_aux() {
     const Tables &T = tables();
     std::vector<uint32_t> aux(kAuxDwords, 0);
@@ -126,6 +165,10 @@ inline std::vector<uint32_t> build_aux() {
         aux[256 + i] = T.inv_top[i];
     }
     for (uint32_t t = 0; t < 5; t++) aux[512 + t] = ~((0xffffffffu >> 8) ^ T.t[0][(0xffffffffu ^ t) & 0xffu]);
+    for (uint32_t t = 0; t < 5; t++) aux[520 + t] = slice4_inv(~aux[512 + t]);
+    aux[525] = slice4_inv(0xffffffffu);
+    for (int j = 0; j < 4; j++)
+        for (uint32_t v = 0; v < 256; v++) aux[528 + 256 * j + v] = slice4_inv(v << (8 * j));
     return aux;
 }
 

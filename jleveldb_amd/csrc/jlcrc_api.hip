@@ -113,7 +113,35 @@ jlk::KParams base_params(const void *d_base, uint64_t n, int mode) {
 
 int run_general(const jlk::KParams &P, hipStream_t st) {
     if (P.n == 0) return JL_OK;
-    JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
+    // A/B knobs (tuning only; defaults are the measured best): JL_GENERAL=stream
+    // selects the step-granular stream kernel (measured slower on C3 so far,
+    // profiles/), JL_STREAM_DEPTH its ring depth (16/32/48)
+    const char *e_g = getenv("JL_GENERAL");
+    const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 32;
+    if (!(e_g && !strcmp(e_g, "stream")) && !getenv("JL_STREAM_DEBUG")) {
+        JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
+        return JL_OK;
+    }
+    if (const char *dbg = getenv("JL_STREAM_DEBUG")) {  // "lo:hi" valid load range (hex), debugging only
+        jlk::KParams Q = P;
+        Q.dbg_lo = strtoull(dbg, nullptr, 16);
+        const char *c = strchr(dbg, ':');
+        Q.dbg_hi = c ? strtoull(c + 1, nullptr, 16) : ~0ull;
+        unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
+        JL_HIP(hipMalloc((void **)&d_dbg, sizeof(h_dbg)));
+        JL_HIP(hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st));
+        Q.dbg = d_dbg;
+        JL_HIP(jlk::launch_stream(ctx().d_img, Q, nullptr, grid_for(P.n), depth, st));
+        JL_HIP(hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st));
+        JL_HIP(hipStreamSynchronize(st));
+        (void)hipFree(d_dbg);
+        fprintf(stderr, "JL_STREAM_DEBUG mode=%d n=%llu bad=%llu\n", P.mode, (unsigned long long)P.n, h_dbg[0]);
+        for (unsigned long long i = 0; i < h_dbg[0] % 1000000ull && i < 256; i++)
+            fprintf(stderr, "  block %llu entry %llu lane %llu addr %llx (base %llx)\n", h_dbg[1 + 4 * i], h_dbg[2 + 4 * i],
+                    h_dbg[3 + 4 * i], h_dbg[4 + 4 * i], (unsigned long long)(uintptr_t)P.base);
+        return JL_OK;
+    }
+    JL_HIP(jlk::launch_stream(ctx().d_img, P, nullptr, grid_for(P.n), depth, st));
     return JL_OK;
 }
 
@@ -386,6 +414,34 @@ int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t
     P.type = d_type;
     P.out8 = d_header;
     return run_general(P, pick(stream));
+}
+
+int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uint64_t *d_frag_src_off,
+                    const uint32_t *d_frag_len, const uint8_t *d_frag_type, uint64_t n_frags, uint64_t log_bytes,
+                    uint8_t *d_log, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (n_frags == 0 && log_bytes == 0) return JL_OK;
+    if (!d_log || (n_frags && (!d_src || !d_frag_hdr_off || !d_frag_src_off || !d_frag_len || !d_frag_type)))
+        return fail(JL_ERR_INVALID, "jl_log_emit_dev: null pointer");
+    Context &c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);  // ws_off holds the payload offsets
+    hipStream_t st = pick(stream);
+    JL_HIP(hipMemsetAsync(d_log, 0, log_bytes, st));  // block trailers (J/db/LogWriter.java:101-107)
+    if (n_frags == 0) return JL_OK;
+    JL_HIP(c.ws_off.ensure(n_frags * 8));
+    uint64_t *pay = (uint64_t *)c.ws_off.p;
+    JL_HIP(jlk::launch_log_copy((const uint8_t *)d_src, d_frag_src_off, d_frag_hdr_off, d_frag_len, n_frags, d_log,
+                                pay, st));
+    jlk::KParams P = base_params(d_log, n_frags, jlk::MODE_LOG_HEADER);
+    P.off = pay;
+    P.len = d_frag_len;
+    P.type = d_frag_type;
+    P.out8 = d_log;
+    P.hdr_off = d_frag_hdr_off;
+    if (int r = run_general(P, st)) return r;
+    // the workspace is reused by the next call: finish before releasing the lock
+    JL_HIP(hipStreamSynchronize(st));
+    return JL_OK;
 }
 
 static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,

@@ -32,6 +32,11 @@ struct KParams {
     int mode;
     uint32_t *out32;
     uint8_t *out8;
+    const uint64_t *hdr_off;  // MODE_LOG_HEADER: header i goes to out8 + hdr_off[i] (null: out8 + 7*i)
+    // debug bounds checking (JL_STREAM_DEBUG): valid load range and a log of
+    // offending accesses {block, entry, lane, address}; dbg == null: off
+    uint64_t dbg_lo, dbg_hi;
+    unsigned long long *dbg;
 };
 
 struct LogEvent {  // layout-identical to jl_log_event
@@ -46,10 +51,16 @@ hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *z
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
+hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
+// one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
+template <int MODE>
+hipError_t launch_stream_m(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
                            const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st);
 hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
                                LogEvent *ev, int checksum, hipStream_t st);
+hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, const uint64_t *frag_hdr_off,
+                           const uint32_t *frag_len, uint64_t n_frags, uint8_t *log, uint64_t *pay_off, hipStream_t st);
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st);
 hipError_t launch_fill_random(void *dst, uint64_t bytes, uint64_t seed, uint64_t first_word, hipStream_t st);
 

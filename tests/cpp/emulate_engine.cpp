@@ -42,6 +42,45 @@ static uint32_t emulate(const std::vector<uint32_t>& img, const uint8_t* base, u
     return ~total;
 }
 
+// The stream kernel's seeding (crc_stream_kernel): no state shift; the seed
+// word W = slice4^-1(~init) is fed as data at virtual bytes [f-4, f): lane l0-1
+// gets W << 8r, the straddling lane l0 gets (LE32 of the first real bytes << 8r)
+// | W >> (32 - 8r); for l0 == 0 lane 63 starts from one gap step of W << 8r.
+static uint32_t gstep_img(const std::vector<uint32_t>& img, uint32_t x, int lane) {
+    uint32_t b = lane & 31;
+    return img[g_dword_index(3, x & 0xff, b)] ^ img[g_dword_index(2, (x >> 8) & 0xff, b)] ^
+           img[g_dword_index(1, (x >> 16) & 0xff, b)] ^ img[g_dword_index(0, x >> 24, b)];
+}
+
+static uint32_t emulate_stream(const std::vector<uint32_t>& img, const uint8_t* base, uint32_t n, uint32_t init) {
+    if (n == 0) return init;
+    const uint32_t W = slice4_inv(~init);
+    uint32_t K = (n + 255) / 256, f = 256 * K - n, l0 = f >> 2, r = f & 3;
+    uint32_t total = 0;
+    for (int lane = 0; lane < 64; lane++) {
+        uint32_t s = (l0 == 0 && lane == 63) ? gstep_img(img, W << (8 * r), lane) : 0u;
+        for (uint32_t k = 0; k < K; k++) {
+            int64_t p = 256 * (int64_t)k + 4 * lane - f;
+            uint32_t w = 0;
+            if (p >= 0) memcpy(&w, base + p, 4);
+            if (k == 0 && (uint32_t)lane == l0 && r) {
+                uint32_t dw = 0;
+                memcpy(&dw, base, n < 4 ? n : 4);
+                w = (dw << (8 * r)) | (W >> (32 - 8 * r));
+            }
+            if (k == 0 && l0 > 0 && (uint32_t)lane == l0 - 1) w = W << (8 * r);
+            s = gstep_img(img, s ^ w, lane);
+        }
+        uint32_t c = 0;
+        for (int j = 0; j < 8; j++) {
+            uint32_t v = (s >> (4 * j)) & 15;
+            c ^= img[32768 + (((lane >> 5) * 8 + j) * 16 + v) * 32 + (lane & 31)];
+        }
+        total ^= c;
+    }
+    return ~total;
+}
+
 int main() {
     auto img = build_lds_image();
     std::mt19937_64 rng(42);
@@ -53,8 +92,10 @@ int main() {
             uint32_t init = (n % 3 == 0) ? 0 : (uint32_t)rng();
             uint32_t want = ~ref_update(~init, buf.data() + a, n);
             uint32_t got = emulate(img, buf.data() + a, n, init);
+            uint32_t got2 = emulate_stream(img, buf.data() + a, n, init);
             cases++;
             if (want != got && bad++ < 5) printf("mismatch n=%u a=%d %08x %08x\n", n, a, want, got);
+            if (want != got2 && bad++ < 5) printf("stream mismatch n=%u a=%d %08x %08x\n", n, a, want, got2);
         }
     }
     for (uint32_t n : {4096u, 4097u, 8191u, 65536u, 65535u, 32768u, 65000u}) {

@@ -123,3 +123,29 @@ def test_engine_math_emulation():
     r = subprocess.run([exe], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+
+
+# --- LogWriter.addRecord framing plan (host C++, no device work) -----------
+def _records(seed, n):
+    rng = np.random.default_rng(seed)
+    lens = rng.choice([0, 1, 6, 7, 100, 1056, 32761, 32762, 40000, 100000], size=n).astype(np.uint32)
+    payloads = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in lens]
+    return payloads, lens
+
+
+@pytest.mark.parametrize("dest_length", [0, 32768 - 7, 32768 - 3, 5000])
+def test_log_layout_matches_logwriter(jl, oracle, dest_length):
+    payloads, lens = _records(dest_length + 1, 60)
+    offs = np.zeros(lens.size, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    plan = jl.log_layout(offs, lens, dest_length)
+    ref = oracle.log_write(payloads, dest_length)
+    assert plan["log_bytes"] == len(ref)
+    src = b"".join(payloads)
+    img = bytearray(len(ref))
+    for h, so, n, t in zip(plan["hdr_off"], plan["src_off"], plan["len"], plan["type"]):
+        h, so, n = int(h), int(so), int(n)
+        assert ref[h + 4] | (ref[h + 5] << 8) == n and ref[h + 6] == t
+        img[h:h + 7] = ref[h:h + 7]  # CRC bytes are the device's job; framing is checked here
+        img[h + 7:h + 7 + n] = src[so:so + n]
+    assert bytes(img) == ref  # everything outside the fragments is zero trailer

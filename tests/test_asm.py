@@ -1,0 +1,45 @@
+"""Build-time guard for the hand-pipelined loads (CPU only, no GPU).
+
+Every engine kernel issues its HBM loads as inline asm and waits for them with
+hand-counted s_waitcnt vmcnt(N).  If the compiler copies a ring register
+between the asm load and its wait (dynamic indexing of a rolled loop, a spill,
+a register-allocation copy) the kernel silently reads stale data — r1 hit
+exactly this (s_set_gpr_idx copies in a rolled ring loop).  This compiles every
+kernel translation unit to gfx950 assembly and rejects any such pattern
+(tools/asm_ring_check.py)."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "jleveldb_amd", "csrc")
+UNITS = [("jlcrc_kernels.hip", [])] + [("stream_kernel.hip", [f"-DJL_MODE={m}"]) for m in range(5)]
+
+
+@pytest.fixture(scope="module")
+def asm(tmp_path_factory):
+    d = tmp_path_factory.mktemp("asm")
+
+    def one(i):
+        src, defs = UNITS[i]
+        out = d / f"u{i}.s"
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed",
+                        "--cuda-device-only", "-S", *defs, "-o", str(out), os.path.join(CSRC, src)],
+                       check=True, capture_output=True)
+        return out.read_text()
+
+    with ThreadPoolExecutor(max_workers=min(6, os.cpu_count() or 1)) as ex:
+        return "\n".join(ex.map(one, range(len(UNITS))))
+
+
+def test_no_stale_ring_reads(asm):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from asm_ring_check import check, kernels
+
+    ks = {s: b for s, b in kernels(asm).items() if "crc_" in s}
+    assert sum("crc_stream_kernel" in s for s in ks) >= 15 and any("crc_fixed4k" in s for s in ks)
+    problems = {s: check(b) for s, b in ks.items()}
+    assert not {s: p for s, p in problems.items() if p}

@@ -10,7 +10,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 200 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o p -- python3 tools/sustain.py > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
+  timeout -k 10 200 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o p -- python3 ${DRIVER:-tools/sustain.py} > gpurun_out/${TAG}_p$i.log 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 gpurun_out/${TAG}_p$i.log; exit 1; }
 done <<< "${GROUPS_LIST:-GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD
 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT
