@@ -111,14 +111,73 @@ jlk::KParams base_params(const void *d_base, uint64_t n, int mode) {
     return P;
 }
 
+// weight of a block for the byte-balanced partition: its bytes plus the
+// per-block fixed cost of the stream kernel (seed, re-alignment, result),
+// roughly that of reading 256 B
+struct BlockWeight {
+    uint32_t add;
+    __host__ __device__ uint64_t operator()(uint32_t len) const { return (uint64_t)len + add + 256u; }
+};
+
+// Byte-balanced wave ranges for the stream kernel (stream-ordered scratch:
+// hipMallocAsync / hipFreeAsync on the caller's stream, so concurrent callers
+// on different streams never share it).  Returns nullptr (count split) when the
+// batch is too small to be worth a scan or the blocks have a fixed stride.
+static uint64_t *make_partition(const jlk::KParams &P, uint64_t waves, hipStream_t st, int *rc) {
+    *rc = JL_OK;
+    if (!P.off || P.n < 16 * waves || getenv("JL_NO_PARTITION")) return nullptr;
+    hipcub::TransformInputIterator<uint64_t, BlockWeight, const uint32_t *> it(P.len, BlockWeight{P.len_add});
+    size_t tmp = 0;
+    if (hipcub::DeviceScan::InclusiveSum(nullptr, tmp, it, (uint64_t *)nullptr, (int)P.n, st) != hipSuccess) {
+        *rc = fail(JL_ERR_HIP, "partition scan sizing failed");
+        return nullptr;
+    }
+    void *buf = nullptr;
+    // every sub-buffer 256-B aligned: hipcub carves its temporaries out of
+    // scan_tmp assuming that alignment (an unaligned one overran, r1)
+    const size_t incl_bytes = (P.n * 8 + 255) & ~(size_t)255, part_bytes = ((waves + 1) * 8 + 255) & ~(size_t)255;
+    if (hipMallocAsync(&buf, incl_bytes + part_bytes + tmp, st) != hipSuccess) {
+        *rc = fail(JL_ERR_NOMEM, "partition scratch allocation failed");
+        return nullptr;
+    }
+    uint64_t *incl = (uint64_t *)buf, *part = (uint64_t *)((char *)buf + incl_bytes);
+    void *scan_tmp = (char *)buf + incl_bytes + part_bytes;
+    if (hipcub::DeviceScan::InclusiveSum(scan_tmp, tmp, it, incl, (int)P.n, st) != hipSuccess ||
+        jlk::launch_partition(incl, P.n, waves, part, st) != hipSuccess) {
+        (void)hipFreeAsync(buf, st);
+        *rc = fail(JL_ERR_HIP, "partition failed");
+        return nullptr;
+    }
+    if (getenv("JL_PARTITION_DUMP")) {  // debugging: range sizes of the partition
+        std::vector<uint64_t> h(waves + 1), hi(P.n);
+        (void)hipMemcpyAsync(h.data(), part, (waves + 1) * 8, hipMemcpyDeviceToHost, st);
+        (void)hipMemcpyAsync(hi.data(), incl, P.n * 8, hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        uint64_t mx = 0, mn = ~0ull, bad = 0;
+        for (uint64_t w = 0; w < waves; w++) {
+            if (h[w + 1] < h[w]) bad++;
+            else { mx = std::max(mx, h[w + 1] - h[w]); mn = std::min(mn, h[w + 1] - h[w]); }
+        }
+        fprintf(stderr, "partition n=%llu waves=%llu total=%llu incl[0]=%llu part[1]=%llu part[W-1]=%llu min=%llu max=%llu bad=%llu\n",
+                (unsigned long long)P.n, (unsigned long long)waves, (unsigned long long)hi[P.n - 1],
+                (unsigned long long)hi[0], (unsigned long long)h[1], (unsigned long long)h[waves - 1],
+                (unsigned long long)mn, (unsigned long long)mx, (unsigned long long)bad);
+    }
+    return part;  // == buf + incl_bytes; freed through free_partition
+}
+
+static void free_partition(const jlk::KParams &P, uint64_t *part, hipStream_t st) {
+    if (part) (void)hipFreeAsync((char *)part - ((P.n * 8 + 255) & ~(size_t)255), st);
+}
+
 int run_general(const jlk::KParams &P, hipStream_t st) {
     if (P.n == 0) return JL_OK;
-    // A/B knobs (tuning only; defaults are the measured best): JL_GENERAL=stream
-    // selects the step-granular stream kernel (measured slower on C3 so far,
-    // profiles/), JL_STREAM_DEPTH its ring depth (16/32/48)
+    // A/B knobs (tuning only; defaults are the measured best): JL_GENERAL=chunk
+    // selects the r1 chunked kernel, JL_STREAM_DEPTH the stream kernel's ring
+    // depth (16/32/48), JL_NO_PARTITION the count split instead of bytes
     const char *e_g = getenv("JL_GENERAL");
-    const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 32;
-    if (!(e_g && !strcmp(e_g, "stream")) && !getenv("JL_STREAM_DEBUG")) {
+    const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 16;
+    if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {
         JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
         return JL_OK;
     }
@@ -141,7 +200,13 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
                     h_dbg[3 + 4 * i], h_dbg[4 + 4 * i], (unsigned long long)(uintptr_t)P.base);
         return JL_OK;
     }
-    JL_HIP(jlk::launch_stream(ctx().d_img, P, nullptr, grid_for(P.n), depth, st));
+    const int grid = grid_for(P.n);
+    int rc = JL_OK;
+    uint64_t *part = make_partition(P, (uint64_t)grid * 16, st, &rc);
+    if (rc) return rc;
+    const hipError_t e = jlk::launch_stream(ctx().d_img, P, part, grid, depth, st);
+    free_partition(P, part, st);
+    JL_HIP(e);
     return JL_OK;
 }
 
@@ -175,6 +240,14 @@ int jl_init(int device) {
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
         return fail(JL_ERR_NO_DEVICE, std::string("jl_init: engine is built for gfx950, device is ") + prop.gcnArchName);
     c.cus = prop.multiProcessorCount;
+    {  // keep stream-ordered scratch (partition arrays) in the pool between calls
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t keep = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        (void)hipGetLastError();
+    }
     JL_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     std::vector<uint32_t> img = jlmath::build_lds_image();
     std::vector<uint32_t> aux = jlmath::build_aux();

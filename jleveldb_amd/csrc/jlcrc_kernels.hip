@@ -593,6 +593,24 @@ __global__ __launch_bounds__(256) void log_copy_kernel(const uint8_t *__restrict
     }
 }
 
+// part[w] for every target T_w = ceil(total*w/W), w in [1, W): the first block
+// whose exclusive prefix reaches T_w.  One thread per block sets the targets
+// that fall inside it, (e_i, e_{i+1}] -> w in [floor(e_i W/total)+1, floor(e_{i+1} W/total)].
+__global__ __launch_bounds__(256) void partition_kernel(const uint64_t *__restrict__ incl, uint64_t n, uint64_t W,
+                                                        uint64_t *__restrict__ part) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = incl[n - 1];
+    if (i == 0) {
+        part[0] = 0;
+        part[W] = n;
+    }
+    if (i >= n) return;
+    const uint64_t e0 = i ? incl[i - 1] : 0, e1 = incl[i];
+    uint64_t lo = e0 * W / total + 1, hi = e1 * W / total;
+    if (hi > W - 1) hi = W - 1;
+    for (uint64_t w = lo; w <= hi; w++) part[w] = i + 1;
+}
+
 __global__ void fill_random_kernel(uint64_t *__restrict__ dst, uint64_t words, uint64_t seed, uint64_t first_word) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
@@ -728,6 +746,11 @@ hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks,
     unsigned grid = (unsigned)((n_blocks + 255) / 256);
     hipLaunchKernelGGL(log_walk_kernel, dim3(grid), dim3(256), 0, st, log, size, n_blocks, pass, counts, starts, ev,
                        d_off, d_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, uint64_t *part, hipStream_t st) {
+    hipLaunchKernelGGL(partition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, incl, n, parts, part);
     return hipGetLastError();
 }
 

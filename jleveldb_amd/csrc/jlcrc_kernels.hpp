@@ -57,6 +57,10 @@ template <int MODE>
 hipError_t launch_stream_m(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
                            const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st);
+// Byte-balanced partition of n blocks over `parts` waves for the stream kernel:
+// incl[i] = sum of weights of blocks 0..i (weight = len + per-block overhead);
+// part[w] = first block of wave w (part[0] = 0, part[parts] = n).
+hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, uint64_t *part, hipStream_t st);
 hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
                                LogEvent *ev, int checksum, hipStream_t st);
 hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, const uint64_t *frag_hdr_off,

@@ -101,97 +101,86 @@ __device__ __forceinline__ void ld_vaddr(uint32_t &dst, uint64_t addr) {
     asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
 }
 
-template <int MODE>
-struct StreamPF {  // prefetch cursor: issues one load per ring slot
-    uint64_t b, b_end;
-    uint32_t e;  // entry within block b
-    SDesc d;
-    __device__ __forceinline__ void skip_empty(const KParams &P) {
+// Prefetch cursor.  All state is wave-uniform (SGPRs).  The common case — a
+// step k >= 1 of the current block — is "plain": bump the SGPR base by 256 and
+// issue one SGPR-based load (a few SALU, no VALU, no branch but the counter
+// test).  Everything else (extra entry, first step with per-lane addresses,
+// moving to the next block and its descriptor) is the rare path, taken
+// ex + 1 times per block.
+template <int MODE, bool DBG>
+struct StreamPF {
+    uint64_t b, b_end;  // current block, range end
+    SDesc d;            // descriptor of b
+    uint64_t base;      // next plain step's base address - 256
+    uint32_t plain;     // plain steps left in b
+    uint32_t stage;     // 0: extra entry next, 1: first step next, 2: block done
+    __device__ __forceinline__ void load_block(const KParams &P) {  // b -> next block with entries (or b_end)
         while (b < b_end) {
             d = stream_desc<MODE>(P, b);
-            if (d.K + d.ex) return;
+            if (d.K + d.ex) {
+                stage = d.ex ? 0u : 1u;
+                return;
+            }
             b++;
         }
     }
-    // debug builds: every load address is checked against [dbg_lo, dbg_hi) and
-    // the zero page; an offending one is logged and replaced by the zero page
-    __device__ __forceinline__ uint64_t check(const KParams &P, uint64_t a, uint32_t lane) {
+    __device__ __forceinline__ uint64_t check(const KParams &P, uint64_t a, uint32_t lane) const {
         const uint64_t zp = (uint64_t)(uintptr_t)P.zero;
-        const bool ok = (a >= P.dbg_lo && a + 4 <= P.dbg_hi) || (a >= zp && a + 4 <= zp + 4096);
-        if (!ok) {
-            unsigned long long slot = atomicAdd(P.dbg, 1ull);
-            if (slot < 256) {
-                P.dbg[1 + 4 * slot] = b;
-                P.dbg[2 + 4 * slot] = e;
-                P.dbg[3 + 4 * slot] = lane;
-                P.dbg[4 + 4 * slot] = a;
-            }
-            return zp + 4u * lane;
+        if ((a >= P.dbg_lo && a + 4 <= P.dbg_hi) || (a >= zp && a + 4 <= zp + 4096)) return a;
+        const unsigned long long slot = atomicAdd(P.dbg, 1ull);
+        if (slot < 256) {
+            P.dbg[1 + 4 * slot] = b;
+            P.dbg[2 + 4 * slot] = stage;
+            P.dbg[3 + 4 * slot] = lane;
+            P.dbg[4 + 4 * slot] = a;
         }
-        return a;
+        return zp + 4u * lane;
     }
-    template <bool DBG>
+    __device__ __forceinline__ void rare(uint32_t &dst, const KParams &P, uint32_t lane) {
+        const uint64_t zp = (uint64_t)(uintptr_t)P.zero;
+        if (stage == 2u) {
+            b++;
+            load_block(P);
+        }
+        uint64_t a = zp + lane * 4u;
+        if (b < b_end) {
+            if (stage == 0u) {  // extra: lane 0 = stored crc, lanes 1-2 = aligned dwords of a block < 4 B
+                if (lane == 0u && MODE == MODE_TABLE_VERIFY) a = d.ptr + d.n;  // trailer crc after block || type
+                if (lane == 0u && MODE == MODE_LOG_VERIFY) a = d.ptr - 6u;      // header crc before type || payload
+                const uint64_t al = d.ptr & ~(uint64_t)3;
+                if (d.n < 4u) {
+                    if (lane == 1u) a = al;
+                    if (lane == 2u && al + 4u <= d.ptr + d.n - 1u) a = al + 4u;
+                }
+                stage = 1u;
+            } else {  // first step: lanes before the block read the zero page
+                const uint32_t l0 = d.f >> 2, r = d.f & 3u;
+                a = d.ptr - d.f + lane * 4u;
+                if (lane < l0) a = zp + lane * 4u;
+                if (lane == l0 && r) a = d.n >= 4u ? d.ptr : zp + lane * 4u;
+                base = uni64(d.ptr - d.f);
+                plain = d.K - 1u;
+                stage = 2u;
+            }
+        }
+        ld_vaddr(dst, DBG ? check(P, a, lane) : a);
+        // the lane-dependent selects above make the compiler treat this path's
+        // results as divergent; pin the cursor back to SGPRs so the plain path
+        // stays scalar
+        b = uni64(b);
+        base = uni64(base);
+        plain = uni(plain);
+        stage = uni(stage);
+    }
     __device__ __forceinline__ void issue(uint32_t &dst, const KParams &P, uint32_t lane) {
-        const uint64_t zp = (uint64_t)(uintptr_t)P.zero;
-        if (DBG) {
-            uint64_t a = zp + lane * 4u;
-            if (b < b_end) {
-                const uint32_t k = e - d.ex;
-                if (e < d.ex) {
-                    if (lane == 0u && MODE == MODE_TABLE_VERIFY) a = d.ptr + d.n;
-                    if (lane == 0u && MODE == MODE_LOG_VERIFY) a = d.ptr - 6u;
-                    const uint64_t al = d.ptr & ~(uint64_t)3;
-                    if (d.n < 4u) {
-                        if (lane == 1u) a = al;
-                        if (lane == 2u && al + 4u <= d.ptr + d.n - 1u) a = al + 4u;
-                    }
-                } else if (k == 0u) {
-                    const uint32_t l0 = d.f >> 2, r = d.f & 3u;
-                    a = d.ptr - d.f + lane * 4u;
-                    if (lane < l0) a = zp + lane * 4u;
-                    if (lane == l0 && r) a = d.n >= 4u ? d.ptr : zp + lane * 4u;
-                } else {
-                    a = d.ptr - d.f + 256u * k + lane * 4u;
-                }
-                if (++e == d.K + d.ex) {
-                    e = 0;
-                    b++;
-                    skip_empty(P);
-                }
-            }
-            ld_vaddr(dst, check(P, a, lane));
+        if (__builtin_expect(plain != 0u, 1)) {
+            plain--;
+            base += 256u;
+            if (DBG) ld_vaddr(dst, check(P, base + lane * 4u, lane));
+            else ld_sbase(dst, base, lane * 4u);
             return;
         }
-        if (b >= b_end) {
-            ld_sbase(dst, zp, lane * 4u);
-            return;
-        }
-        const uint32_t k = e - d.ex;  // step (when e >= ex)
-        if (e < d.ex) {
-            // extra entry: lane 0 = stored crc, lanes 1-2 = the aligned dwords of a block < 4 B
-            uint64_t a = zp + lane * 4u;
-            if (lane == 0u && MODE == MODE_TABLE_VERIFY) a = d.ptr + d.n;  // trailer crc after block || type
-            if (lane == 0u && MODE == MODE_LOG_VERIFY) a = d.ptr - 6u;      // header crc before type || payload
-            const uint64_t al = d.ptr & ~(uint64_t)3;
-            if (d.n < 4u) {
-                if (lane == 1u) a = al;
-                if (lane == 2u && al + 4u <= d.ptr + d.n - 1u) a = al + 4u;
-            }
-            ld_vaddr(dst, a);
-        } else if (k == 0u) {
-            const uint32_t l0 = d.f >> 2, r = d.f & 3u;
-            uint64_t a = d.ptr - d.f + lane * 4u;
-            if (lane < l0) a = zp + lane * 4u;
-            if (lane == l0 && r) a = d.n >= 4u ? d.ptr : zp + lane * 4u;
-            ld_vaddr(dst, a);
-        } else {
-            ld_sbase(dst, d.ptr - d.f + 256u * k, lane * 4u);
-        }
-        if (++e == d.K + d.ex) {
-            e = 0;
-            b++;
-            skip_empty(P);
-        }
+        rare(dst, P, lane);
     }
 };
 
@@ -282,17 +271,20 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(const uint4 *__restric
     }
     if (b_begin >= b_end) return;
 
-    StreamPF<MODE> pf;
+    StreamPF<MODE, DBG> pf;
     pf.b = b_begin;
     pf.b_end = b_end;
-    pf.e = 0;
-    pf.skip_empty(P);
-    // The ring is indexed only with literal slot numbers (JL_SLOT below): a ring
-    // register must never be copied between its asm load and its s_waitcnt, so
-    // no loop the compiler might leave rolled may index it (tests/test_asm.py).
+    pf.plain = 0;
+    pf.base = 0;
+    pf.stage = 1;
+    pf.load_block(P);
+    // The ring is indexed only with literal slot numbers (JL_PRE / JL_SLOT): a
+    // ring register must never be copied between its asm load and its
+    // s_waitcnt, so no loop the compiler might leave rolled may index it
+    // (tests/test_asm.py).
     uint32_t ring[P_];
 #define JL_PRE(u) \
-    if constexpr ((u) < P_) pf.template issue<DBG>(ring[u], P, lane);
+    if constexpr ((u) < P_) pf.issue(ring[u], P, lane);
     JL_PRE(0) JL_PRE(1) JL_PRE(2) JL_PRE(3) JL_PRE(4) JL_PRE(5) JL_PRE(6) JL_PRE(7) JL_PRE(8) JL_PRE(9) JL_PRE(10)
     JL_PRE(11) JL_PRE(12) JL_PRE(13) JL_PRE(14) JL_PRE(15) JL_PRE(16) JL_PRE(17) JL_PRE(18) JL_PRE(19) JL_PRE(20)
     JL_PRE(21) JL_PRE(22) JL_PRE(23) JL_PRE(24) JL_PRE(25) JL_PRE(26) JL_PRE(27) JL_PRE(28) JL_PRE(29) JL_PRE(30)
@@ -300,38 +292,51 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(const uint4 *__restric
     JL_PRE(41) JL_PRE(42) JL_PRE(43) JL_PRE(44) JL_PRE(45) JL_PRE(46) JL_PRE(47)
 #undef JL_PRE
 
-    // compute cursor
+    // Compute cursor: plain = middle steps left in the current block; the rare
+    // path handles the extra entry (stage 0), the first step with its seed
+    // (stage 1) and the last step with the block's result (stage 2).
     uint64_t cb = b_begin;
-    uint32_t ce = 0;
     SDesc cd = stream_desc<MODE>(P, cb);
+    uint32_t plain = 0, stage = cd.ex ? 0u : 1u;
     uint32_t t = 0, v3 = 0, stored = 0, tiny = 0;
     StreamFin F;
     F.fin0 = b_begin;
 
-    // moves cb past block cb and any empty blocks after it (their results are
-    // recorded); false when the range is done
+    // cb -> next block with entries, recording empty blocks on the way; false when done
     auto advance = [&]() -> bool {
         for (;;) {
-            if (++cb >= b_end) return false;
+            cb++;
+            if (cb >= b_end) return false;
             cd = stream_desc<MODE>(P, cb);
-            if (cd.K + cd.ex) return true;
+            if (cd.K + cd.ex) {
+                stage = cd.ex ? 0u : 1u;
+                return true;
+            }
             stream_result<MODE>(P, F, cb, cd, ~stream_init<MODE>(P, cb), 0u, lane);
         }
     };
-    // one ring entry of the compute cursor; false when the range is done
-    auto consume = [&](uint32_t wv) -> bool {
-        if (ce < cd.ex) {  // extra entry: stored crc (lane 0), bytes of a block < 4 B (lanes 1-2)
+    auto step = [&](uint32_t word) {
+        const uint32_t x = xor3(t, v3, word);
+        const uint32_t a0 = lds_at(lds, JL_GADDR(gl.l3, x, 0u));
+        const uint32_t a1 = lds_at(lds, JL_GADDR(gl.l2, x, 1u));
+        const uint32_t a2 = lds_at(lds, JL_GADDR(gl.l1, x, 2u));
+        v3 = lds_at(lds, JL_GADDR(gl.l0, x, 3u));
+        t = xor3(a0, a1, a2);
+    };
+    // rare entry of the compute cursor; false when the range is done
+    auto rare = [&](uint32_t wv) -> bool {
+        if (stage == 0u) {  // extra entry
             stored = uni(wv);
             if (cd.n < 4u) {
                 const uint32_t d1 = (uint32_t)__builtin_amdgcn_readlane((int)wv, 1);
                 const uint32_t d2 = (uint32_t)__builtin_amdgcn_readlane((int)wv, 2);
                 tiny = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)(cd.ptr & 3u)) & (0xffffffffu >> (32 - 8 * cd.n));
             }
-            ce++;
+            stage = 1u;
             return true;
         }
         uint32_t word = wv;
-        if (ce == cd.ex) {  // first step: seed word W fed as the 4 bytes before the block
+        if (stage == 1u) {  // first step: seed word W fed as the 4 bytes before the block
             const uint32_t W = stream_seed<MODE>(P, cb);
             const uint32_t l0 = cd.f >> 2, r = cd.f & 3u, sh = 8u * r;
             if (r && lane == l0) word = ((cd.n >= 4u ? wv : tiny) << sh) | (W >> (32u - sh));
@@ -342,17 +347,24 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(const uint4 *__restric
                 const uint32_t s63 = gstep(lds, W << sh, gl);
                 t = lane == 63u ? s63 : 0u;
             }
+            step(word);
+            if (cd.K > 1u) {
+                plain = cd.K - 2u;
+                stage = 2u;
+                return true;
+            }
+        } else {
+            step(word);  // last step
         }
-        const uint32_t x = xor3(t, v3, word);
-        const uint32_t a0 = lds_at(lds, JL_GADDR(gl.l3, x, 0u));
-        const uint32_t a1 = lds_at(lds, JL_GADDR(gl.l2, x, 1u));
-        const uint32_t a2 = lds_at(lds, JL_GADDR(gl.l1, x, 2u));
-        v3 = lds_at(lds, JL_GADDR(gl.l0, x, 3u));
-        t = xor3(a0, a1, a2);
-        if (++ce < cd.K + cd.ex) return true;
-        ce = 0;
         stream_result<MODE>(P, F, cb, cd, wave_xor(realign(lds, t ^ v3, lc)), stored, lane);
         return advance();
+    };
+    auto rare_pinned = [&](uint32_t wv) -> bool {  // as in StreamPF::rare: keep the cursor in SGPRs
+        const bool more = rare(wv);
+        plain = uni(plain);
+        stage = uni(stage);
+        cb = uni64(cb);
+        return more;
     };
     if (cd.K + cd.ex == 0) {
         stream_result<MODE>(P, F, cb, cd, ~stream_init<MODE>(P, cb), 0u, lane);
@@ -363,8 +375,13 @@ __global__ __launch_bounds__(1024) void crc_stream_kernel(const uint4 *__restric
 #define JL_SLOT(u)                                                               \
     if constexpr ((u) < P_) {                                                    \
         asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ring[u]) : "n"(P_ - 1));       \
-        if (!consume(ring[u])) goto drain;                                       \
-        pf.template issue<DBG>(ring[u], P, lane);                                \
+        if (__builtin_expect(plain != 0u, 1)) {                                  \
+            plain--;                                                             \
+            step(ring[u]);                                                       \
+        } else if (!rare_pinned(ring[u])) {                                      \
+            goto drain;                                                          \
+        }                                                                        \
+        pf.issue(ring[u], P, lane);                                              \
     }
         JL_SLOT(0) JL_SLOT(1) JL_SLOT(2) JL_SLOT(3) JL_SLOT(4) JL_SLOT(5) JL_SLOT(6) JL_SLOT(7) JL_SLOT(8)
         JL_SLOT(9) JL_SLOT(10) JL_SLOT(11) JL_SLOT(12) JL_SLOT(13) JL_SLOT(14) JL_SLOT(15) JL_SLOT(16)
@@ -378,7 +395,6 @@ drain:
     stream_flush<MODE>(P, F, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-
 
 template <>
 hipError_t launch_stream_m<JL_MODE>(const void *img, const KParams &P, const uint64_t *part, int grid, int depth,

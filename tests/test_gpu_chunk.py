@@ -1,6 +1,6 @@
-"""The step-granular stream kernel (JL_GENERAL=stream) against the oracle: the
-variable-size, table and log parity cases of test_gpu_parity.py re-run with the
-stream kernel selected."""
+"""The r1 chunked kernel (JL_GENERAL=chunk, kept for A/B) against the oracle: the
+variable-size, table and log parity cases of test_gpu_parity.py re-run with it
+selected (the default is the stream kernel)."""
 import pytest
 
 import test_gpu_parity as base
@@ -9,35 +9,33 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def stream_kernel(monkeypatch):
-    monkeypatch.setenv("JL_GENERAL", "stream")
+def chunk_kernel(monkeypatch):
+    monkeypatch.setenv("JL_GENERAL", "chunk")
 
 
-@pytest.mark.parametrize("depth", ["16", "32", "48"])
-def test_stream_every_length_and_alignment(gpu, jl, oracle, monkeypatch, depth):
-    monkeypatch.setenv("JL_STREAM_DEPTH", depth)
+def test_chunk_every_length_and_alignment(gpu, jl, oracle):
     base.test_batch_every_length_and_alignment(gpu, jl, oracle)
 
 
-def test_stream_large_and_zipf(gpu, jl, oracle):
+def test_chunk_large_and_zipf(gpu, jl, oracle):
     base.test_batch_large_and_zipf(gpu, jl, oracle)
 
 
-def test_stream_golden_fixture(gpu, jl, golden):
+def test_chunk_golden_fixture(gpu, jl, golden):
     base.test_batch_golden_fixture(gpu, jl, golden)
 
 
-def test_stream_fixed_other_sizes(gpu, jl, oracle):
+def test_chunk_fixed_other_sizes(gpu, jl, oracle):
     for bb in (1, 3, 7, 255, 256, 1000, 4097, 100003):
         base.test_fixed_other_sizes(gpu, jl, oracle, bb)
 
 
-def test_stream_table(gpu, jl, oracle, golden):
+def test_chunk_table(gpu, jl, oracle, golden):
     base.test_table_trailers_and_verify(gpu, jl, oracle, golden)
     base.test_table_many_blocks(gpu, jl, oracle)
 
 
-def test_stream_log(gpu, jl, oracle, golden):
+def test_chunk_log(gpu, jl, oracle, golden):
     base.test_log_golden(gpu, jl, oracle, golden)
     base.test_log_random_with_corruption(gpu, jl, oracle, 3)
     base.test_log_special_records(gpu, jl, oracle)

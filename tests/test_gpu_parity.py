@@ -84,6 +84,16 @@ def test_batch_every_length_and_alignment(gpu, jl, oracle):
     assert np.array_equal(got, oracle.batch(arena, off, ln, suffix=sfx, threads=THREADS))
 
 
+@pytest.mark.parametrize("depth,partition", [("32", True), ("48", False), ("16", False)])
+def test_stream_depths_and_partition(gpu, jl, oracle, monkeypatch, depth, partition):
+    """Stream-kernel ring depths (JL_STREAM_DEPTH) and the count split (JL_NO_PARTITION)."""
+    monkeypatch.setenv("JL_STREAM_DEPTH", depth)
+    if not partition:
+        monkeypatch.setenv("JL_NO_PARTITION", "1")
+    test_batch_every_length_and_alignment(gpu, jl, oracle)
+    test_batch_large_and_zipf(gpu, jl, oracle)
+
+
 def test_batch_large_and_zipf(gpu, jl, oracle):
     rng = np.random.default_rng(12)
     ks = rng.zipf(1.1, 20000)

@@ -17,7 +17,7 @@ torch.cuda.set_device(0)
 jl.init(0)
 dev = torch.device("cuda:0")
 rounds = int(os.environ.get("ROUNDS", 3))
-variants = os.environ.get("VARIANTS", "chunk s16 s32 s48").split()
+variants = os.environ.get("VARIANTS", "chunk s16np s16 s32").split()
 
 # C3
 rng = np.random.default_rng(SEED)
@@ -46,11 +46,22 @@ log = jl.log_emit_dev(src, plan)
 del src
 events = torch.empty((log.numel() // 7 + 2) * 16, dtype=torch.uint8, device=dev)
 
+# C2 through the general path (1M x 4 KiB blocks described by off/len arrays)
+n2 = 1 << 20
+arena2 = torch.empty(n2 * 4096, dtype=torch.uint8, device=dev)
+jl.fill_random_dev(arena2, SEED)
+off2 = torch.arange(n2, dtype=torch.int64, device=dev) * 4096
+len2 = torch.full((n2,), 4096, dtype=torch.int32, device=dev)
+out2 = torch.empty(n2, dtype=torch.int32, device=dev)
+
 
 def setv(v):
     os.environ["JL_GENERAL"] = "chunk" if v == "chunk" else "stream"
+    os.environ.pop("JL_NO_PARTITION", None)
     if v != "chunk":
-        os.environ["JL_STREAM_DEPTH"] = v[1:]
+        os.environ["JL_STREAM_DEPTH"] = v[1:].replace("np", "")
+        if v.endswith("np"):
+            os.environ["JL_NO_PARTITION"] = "1"
 
 
 def t_of(fn, reps=5):
@@ -66,7 +77,7 @@ def t_of(fn, reps=5):
 
 
 ref3 = ref5 = None
-times = {v: {"c3": [], "c5": []} for v in variants}
+times = {v: {"c3": [], "c5": [], "c2": []} for v in variants}
 for r in range(rounds):
     for v in variants:
         setv(v)
@@ -80,10 +91,12 @@ for r in range(rounds):
         assert np.array_equal(ref5, got5), ("C5 mismatch", v)
         times[v]["c3"].append(t_of(lambda: jl.crc32c_batch_dev(arena, d_off, d_len, out=out)))
         times[v]["c5"].append(t_of(lambda: jl.log_verify_dev(log, events=events)))
+        times[v]["c2"].append(t_of(lambda: jl.crc32c_batch_dev(arena2, off2, len2, out=out2)))
 kinds5 = ref5.reshape(-1, 16)[:, 13]
 print(json.dumps({"c5_records": int(ne), "c5_ok": int((kinds5 == 1).sum())}))
 for v in variants:
     c3 = float(np.median(times[v]["c3"]))
     c5 = float(np.median(times[v]["c5"]))
     print(json.dumps({"variant": v, "c3_ms": round(c3, 3), "c3_GBps": round((total + 16 * n) / (c3 / 1e3) / 1e9, 1),
-                      "c5_ms": round(c5, 3), "c5_GiBps": round(log.numel() / (c5 / 1e3) / 2**30, 1)}))
+                      "c5_ms": round(c5, 3), "c5_GiBps": round(log.numel() / (c5 / 1e3) / 2**30, 1),
+                      "c2_general_ms": round(float(np.median(times[v]["c2"])), 3)}))
