@@ -10,7 +10,7 @@ C4 8M-block set, generated in place (weak scaling, no data-path collective);
 value = all ranks' bytes / max-over-ranks time.
 
 Also reported on the same JSON line:
-  roofline     — dominant kernel (crc_fixed4k_x2_kernel) timed with HIP events on
+  roofline     — dominant kernel (crc_fixed4k_v4_kernel) timed with HIP events on
                  its launch stream; algorithmic bytes = 4096 B read + 4 B
                  written per block; peak = 8.0 TB/s (MI355X spec);
                  measured read-stream ceiling beside it; traffic from the
@@ -64,7 +64,7 @@ def read_stream_ceiling(data, stream) -> float:
 
 
 def pmc_traffic():
-    """HBM bytes per launch of crc_fixed4k_kernel from the committed PMC summary."""
+    """HBM bytes per launch of the 4 KiB kernel from the committed PMC summary."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*fixed4k*.json")))
     if not files:
         return None, None
@@ -277,7 +277,7 @@ def main():
                        "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "crc_fixed4k_x2_kernel<nt, bitop3>",
+                "kernel": "crc_fixed4k_v4_kernel<8 lanes/block, nt>",
                 "achieved": round(achieved, 1),
                 "peak": PEAK_GBS,
                 "unit": "GB/s",

@@ -16,6 +16,7 @@
 
 static_assert(jlmath::kImageBytes == jlk::kImageBytes, "LDS image size mismatch");
 static_assert(sizeof(jl_log_event) == sizeof(jlk::LogEvent), "event layout mismatch");
+static_assert(jlmath::kV4SlotDword == jlk::kV4SlotDword && jlmath::kV4UDword * 4 == jlk::kV4U4Byte, "v4 image layout mismatch");
 
 namespace {
 
@@ -61,6 +62,7 @@ struct Context {
     int cus = 0;
     hipStream_t stream = nullptr;
     void *d_img = nullptr;   // 160 KiB LDS image
+    void *d_img_v4[3] = {nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block
     uint32_t *d_aux = nullptr;
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
@@ -256,6 +258,11 @@ int jl_init(int device) {
     JL_HIP(hipMalloc((void **)&c.d_zero, 4096));
     JL_HIP(hipMalloc((void **)&c.d_scratch, 4096));
     JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
+    for (int i = 0; i < 3; i++) {
+        std::vector<uint32_t> v4 = jlmath::build_lds_image_v4(4 << i);
+        JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
+        JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
+    }
     JL_HIP(hipMemcpy(c.d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice));
     JL_HIP(hipMemset(c.d_zero, 0, 4096));
     c.device = device;
@@ -281,6 +288,10 @@ int jl_shutdown(void) {
         sl = Context::Slot();
     }
     (void)hipFree(c.d_img);
+    for (void *&p : c.d_img_v4) {
+        (void)hipFree(p);
+        p = nullptr;
+    }
     (void)hipFree(c.d_aux);
     (void)hipFree(c.d_zero);
     (void)hipFree(c.d_scratch);
@@ -308,7 +319,13 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
         const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH"), *e_c = getenv("JL_FIXED_CHAINS");
         const int nt = e_nt ? atoi(e_nt) : 1;
         const int depth = e_d ? atoi(e_d) : 2;
-        const int chains = e_c ? atoi(e_c) : 3;
+        const int chains = e_c ? atoi(e_c) : 7;  // 7 = v4 (fixed_v4.hip), measured best
+        if ((chains == 7 || chains == 8 || chains == 10) && ((uintptr_t)d_data & 15) == 0) {  // v4 path: 7 = 8 lanes/block, 8 = 16, 10 = 8 without nt
+            const int lpb = chains == 8 ? 16 : 8;
+            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[lpb == 4 ? 0 : lpb == 8 ? 1 : 2], (const uint8_t *)d_data,
+                                          n_blocks, flags, d_out, grid_for(n_blocks), lpb, chains != 10, st));
+            return JL_OK;
+        }
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
                                    ctx().d_scratch, grid_for(n_blocks), nt, depth, chains, st));
         return JL_OK;

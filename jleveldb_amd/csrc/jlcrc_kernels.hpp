@@ -7,6 +7,9 @@
 namespace jlk {
 
 constexpr uint32_t kImageBytes = 163840;  // must equal jlmath::kImageBytes
+// v4 image (fixed_v4.hip, crc_math.hpp build_lds_image_v4): region B offsets
+constexpr uint32_t kV4U4Byte = 147456;   // uniform z^-4, z^-8, z^-12 nibble tables (512 B each)
+constexpr uint32_t kV4SlotDword = 37248; // per-wave result slots (64 dwords per wave)
 
 enum : int {
     MODE_CRC = 0,           // out32[i] = crc / mask(crc)
@@ -50,6 +53,9 @@ struct LogEvent {  // layout-identical to jl_log_event
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st);
+// v4 fast path (fixed_v4.hip): lpb = lanes per block (8, 16); img = the v4 image for that lpb
+hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
+                             int grid, int lpb, int nt, hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)

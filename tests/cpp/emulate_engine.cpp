@@ -81,6 +81,36 @@ static uint32_t emulate_stream(const std::vector<uint32_t>& img, const uint8_t* 
     return ~total;
 }
 
+// The v4 fixed kernel (fixed_v4.hip): LPB lanes per 4 KiB block, lane l' reads
+// 16 B at 16*LPB*k + 16*l'; dword j feeds chain j through gap tables
+// z^(16*LPB-4+t); chains folded with the uniform z^-4j tables, the lane with
+// z^-(16 l') (bank copy b = lane & 31), lanes XORed.
+static uint32_t emulate_v4(const std::vector<uint32_t>& img, const uint8_t* blk, int lpb, int lane_base) {
+    const int step = 16 * lpb, S = 4096 / step;
+    uint32_t total = 0;
+    for (int lp = 0; lp < lpb; lp++) {
+        const int lane = lane_base + lp, b = lane & 31;
+        uint32_t s[4];
+        for (int j = 0; j < 4; j++) {
+            s[j] = (lp == 0 && j == 0) ? 0xffffffffu : 0u;
+            for (int k = 0; k < S; k++) {
+                uint32_t w;
+                memcpy(&w, blk + step * k + 16 * lp + 4 * j, 4);
+                uint32_t x = s[j] ^ w;
+                s[j] = img[g_dword_index(3, x & 0xff, b)] ^ img[g_dword_index(2, (x >> 8) & 0xff, b)] ^
+                       img[g_dword_index(1, (x >> 16) & 0xff, b)] ^ img[g_dword_index(0, x >> 24, b)];
+            }
+        }
+        uint32_t c = s[0];
+        for (int u = 0; u < 3; u++)
+            for (int p = 0; p < 8; p++) c ^= img[kV4UDword + u * 128 + p * 16 + ((s[u + 1] >> (4 * p)) & 15)];
+        uint32_t r = 0;
+        for (int p = 0; p < 8; p++) r ^= img[32768 + (p * 16 + ((c >> (4 * p)) & 15)) * 32 + b];
+        total ^= r;
+    }
+    return ~total;
+}
+
 int main() {
     auto img = build_lds_image();
     std::mt19937_64 rng(42);
@@ -103,6 +133,16 @@ int main() {
         uint32_t got = emulate(img, buf.data() + 1, n, 0);
         cases++;
         if (want != got && bad++ < 10) printf("mismatch n=%u %08x %08x\n", n, want, got);
+    }
+    for (int lpb : {8, 16}) {
+        auto img4 = build_lds_image_v4(lpb);
+        for (int q = 0; q < 64 / lpb; q++) {
+            const uint8_t* blk = buf.data() + 4096 * (q % 16);
+            uint32_t want = ~ref_update(~0u, blk, 4096);
+            uint32_t got = emulate_v4(img4, blk, lpb, q * lpb);
+            cases++;
+            if (want != got && bad++ < 10) printf("v4 mismatch lpb=%d q=%d %08x %08x\n", lpb, q, want, got);
+        }
     }
     printf("%d cases, %d mismatches\n", cases, bad);
     return bad != 0;

@@ -16,7 +16,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "jleveldb_amd", "csrc")
-UNITS = [("jlcrc_kernels.hip", [])] + [("stream_kernel.hip", [f"-DJL_MODE={m}"]) for m in range(5)]
+UNITS = [("jlcrc_kernels.hip", []), ("fixed_v4.hip", [])] + [("stream_kernel.hip", [f"-DJL_MODE={m}"]) for m in range(5)]
 
 
 @pytest.fixture(scope="module")
@@ -40,6 +40,6 @@ def test_no_stale_ring_reads(asm):
     from asm_ring_check import check, kernels
 
     ks = {s: b for s, b in kernels(asm).items() if "crc_" in s}
-    assert sum("crc_stream_kernel" in s for s in ks) >= 15 and any("crc_fixed4k" in s for s in ks)
+    assert sum("crc_stream_kernel" in s for s in ks) >= 15 and any("crc_fixed4k_x2" in s for s in ks) and any("crc_fixed4k_v4" in s for s in ks)
     problems = {s: check(b) for s, b in ks.items()}
     assert not {s: p for s, p in problems.items() if p}

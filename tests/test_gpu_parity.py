@@ -36,6 +36,33 @@ def test_fixed_4k_random(gpu, jl, oracle, n_blocks):
     assert np.array_equal(raw, oracle.fixed(host, 4096, n_blocks, flags=0, threads=THREADS))
 
 
+FIXED_VARIANTS = {"x2": "3", "x2plain": "2", "v4_8": "7", "v4_16": "8", "v4_8_plain": "10"}
+
+
+@pytest.mark.parametrize("variant", sorted(FIXED_VARIANTS))
+@pytest.mark.parametrize("n_blocks", [1, 7, 8, 9, 63, 64, 65, 1000, 16385, 65536 + 13])
+def test_fixed_4k_kernel_variants(gpu, jl, oracle, monkeypatch, variant, n_blocks):
+    """Every 4 KiB kernel variant (JL_FIXED_CHAINS), ragged counts around the
+    round (8/4 blocks), group (64 blocks) and grid boundaries."""
+    monkeypatch.setenv("JL_FIXED_CHAINS", FIXED_VARIANTS[variant])
+    rng = np.random.default_rng(1000 + n_blocks)
+    host = rng.integers(0, 256, n_blocks * 4096, dtype=np.uint8)
+    d = to_dev(host, gpu)
+    for flags in (1, 0):
+        got = u32(jl.crc32c_fixed_dev(d, 4096, flags=flags))
+        assert np.array_equal(got, oracle.fixed(host, 4096, n_blocks, flags=flags, threads=THREADS)), flags
+
+
+def test_fixed_4k_v4_out_of_place_views(gpu, jl, oracle, monkeypatch):
+    """v4 kernel on a sub-view (unaligned-to-group base, block count not a round multiple)."""
+    monkeypatch.setenv("JL_FIXED_CHAINS", "7")
+    rng = np.random.default_rng(77)
+    host = rng.integers(0, 256, 300 * 4096, dtype=np.uint8)
+    d = to_dev(host, gpu)
+    got = u32(jl.crc32c_fixed_dev(d[5 * 4096:], 4096, 290))
+    assert np.array_equal(got, oracle.fixed(host[5 * 4096:], 4096, 290, threads=THREADS))
+
+
 def test_fixed_4k_dbbench_x(gpu, jl, golden):
     """DBBench.crc32c input (J/benchmark/DBBench.java:775-793): 4096 x 'x'."""
     d = to_dev(np.frombuffer(b"x" * 4096 * 3, dtype=np.uint8), gpu)

@@ -30,36 +30,54 @@ def kernels(text):
 
 
 def check(body):
+    """Linear scan of the kernel text, twice (the second pass models a loop back
+    edge carrying loads issued at the end of a loop body into its head).  Pending
+    asm loads complete in issue order: `s_waitcnt vmcnt(N)` retires all but the
+    N most recent.  Labels do NOT reset the state (a ring's loads cross blocks)."""
     problems = []
     if re.search(r"s_set_gpr_idx_on|v_movrel|scratch_|buffer_store_dword .*off, s\[0:3\]", body):
         problems.append("dynamic GPR indexing or scratch access")
-    pending = {}
-    for l in body.split("\n"):
-        t = l.strip()
-        if not t or t.startswith(";"):
-            continue
-        if re.match(r"\.LBB|^\S+:", t):
-            pending = {}
-            continue
-        m = re.match(r"global_load_dword (v\d+),", t)
-        if m:
-            pending[int(m.group(1)[1:])] = t
-            continue
-        if t.startswith("s_waitcnt") and "vmcnt" in t:
-            pending = {}
-            continue
-        parts = t.split(None, 1)
-        if len(parts) < 2:
-            continue
-        ops = parts[1].split(",")
-        store = parts[0].startswith(("global_store", "ds_write", "buffer_store", "flat_store"))
-        srcs = _regs(parts[1]) if store else _regs(",".join(ops[1:]))
-        dst = set() if store else _regs(ops[0])
-        for v in list(pending):
-            if v in srcs:
-                problems.append(f"v{v} read before its wait: {t}")
-            elif v in dst:
-                del pending[v]
+    lines = [l.strip() for l in body.split("\n")]
+    pending = []  # [(regs, instr)] in issue order
+    seen = set()
+    for pas in range(2):
+        for t in lines:
+            if not t or t.startswith((";", ".")) or re.match(r"^\S+:$", t):
+                continue
+            m = re.match(r"(?:global|buffer)_load_dword(?:x\d)? (v\d+|v\[\d+:\d+\]),", t)
+            if m:
+                regs = _regs(m.group(1))
+                pending = [(r, i) for r, i in pending if not (r & regs)]
+                pending.append((regs, t))
+                continue
+            w = re.match(r"s_waitcnt .*vmcnt\((\d+)\)", t)
+            if w:
+                n = int(w.group(1))
+                pending = pending[len(pending) - n:] if n < len(pending) else pending
+                if n == 0:
+                    pending = []
+                continue
+            parts = t.split(None, 1)
+            if len(parts) < 2:
+                continue
+            ops = parts[1].split(",")
+            store = parts[0].startswith(("global_store", "ds_write", "buffer_store", "flat_store"))
+            srcs = _regs(parts[1]) if store else _regs(",".join(ops[1:]))
+            dst = set() if store else _regs(ops[0])
+            mad = re.match(r"v_mad_[ui]64_[ui]32 v\[(\d+):(\d+)\], [^,]+, [^,]+, [^,]+, v\[(\d+):(\d+)\]", t)
+            if mad:  # the addend's high dword only reaches the result's high dword: taint it, do not flag
+                hi_src, hi_dst = int(mad.group(4)), int(mad.group(2))
+                hit = [ld for r, ld in pending if hi_src in r]
+                if hit:
+                    srcs = srcs - {hi_src}
+                    dst = dst - {hi_dst}
+                    pending = [(r - {hi_dst}, i) for r, i in pending if r - {hi_dst}] + [({hi_dst}, hit[0])]
+            for regs, ld in pending:
+                if regs & srcs and t not in seen:
+                    seen.add(t)
+                    problems.append(f"v{sorted(regs & srcs)} read before its wait: {t}  (load: {ld})")
+            # a register overwritten by another instruction no longer holds the load's data
+            pending = [(r - dst, i) for r, i in pending if r - dst]
     return problems
 
 
