@@ -114,36 +114,6 @@ inline std::vector<uint32_t> build_lds_image() {
     return img;
 }
 
-// v4 image (fixed_v4.hip): lanes-per-block LPB, block-step STEP = 16*LPB bytes.
-// Region A: the gap tables of chain dwords STEP bytes apart,
-//   G_t[i] = z^(STEP-4+t)(T0[i]), same addressing as build_lds_image().
-// Region B (dwords):
-//   [32768, 36864)  per-lane shift z^-(16*(b % LPB)) as 8 nibble tables, copy b
-//                   in bank b: dword 32768 + (p*16 + v)*32 + b   (realign() layout)
-//   [36864, 37248)  uniform z^-4, z^-8, z^-12: dword 36864 + u*128 + p*16 + v
-//   [37248, 38272)  per-wave result slots (64 dwords x 16 waves)
-constexpr size_t kV4UDword = 36864;
-constexpr size_t kV4SlotDword = 37248;
-inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
-    const Tables &T = tables();
-    const int gap = 16 * lpb - 4;
-    std::vector<uint32_t> img(kImageDwords, 0);
-    for (int t = 0; t < 4; t++)
-        for (int i = 0; i < 256; i++) {
-            uint32_t g = T.zn(T.t[0][i], (uint64_t)gap + t);
-            for (int b = 0; b < 32; b++) img[g_dword_index(t, i, b)] = g;
-        }
-    for (int b = 0; b < 32; b++)
-        for (int p = 0; p < 8; p++)
-            for (int v = 0; v < 16; v++)
-                img[32768 + (size_t)(p * 16 + v) * 32 + b] = T.zinvn((uint32_t)v << (4 * p), 16u * (uint32_t)(b % lpb));
-    for (int u = 0; u < 3; u++)
-        for (int p = 0; p < 8; p++)
-            for (int v = 0; v < 16; v++)
-                img[kV4UDword + (size_t)u * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 4u * (uint32_t)(u + 1));
-    return img;
-}
-
 // slice4(x) = state after feeding the 4 LE bytes of x to a zero state
 // (T3[x0] ^ T2[x1] ^ T1[x2] ^ T0[x3]); linear and invertible over GF(2).
 inline uint32_t slice4(uint32_t x) {
@@ -177,6 +147,43 @@ inline uint32_t slice4_inv(uint32_t y) {
     for (int i = 0; i < 32; i++)
         if ((y >> i) & 1u) x ^= cols[i];
     return x;
+}
+
+// v4 image (fixed_v4.hip): lanes-per-block LPB, block-step STEP = 16*LPB bytes.
+// Region A: the gap tables of chain dwords STEP bytes apart,
+//   G_t[i] = z^(STEP-4+t)(T0[i]), same addressing as build_lds_image().
+// Region B (dwords):
+//   [32768, 36864)  per-lane shift z^-(16*(b % LPB)) as 8 nibble tables, copy b
+//                   in bank b: dword 32768 + (p*16 + v)*32 + b   (realign() layout)
+//   [36864, 37248)  uniform z^-4, z^-8, z^-12: dword 36864 + u*128 + p*16 + v
+//   [37248, 38272)  per-wave result slots (64 dwords x 16 waves)
+//   [38272, 39296)  U_j[v] = slice4^-1(v << 8j), j = 0..3 (general_v4.hip: seed of an init)
+//   [39296, 39552)  T0 (general_v4.hip: suffix byte)
+constexpr size_t kV4UDword = 36864;
+constexpr size_t kV4SlotDword = 37248;
+constexpr size_t kG4UDword = 38272;
+constexpr size_t kG4T0Dword = 39296;
+inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
+    const Tables &T = tables();
+    const int gap = 16 * lpb - 4;
+    std::vector<uint32_t> img(kImageDwords, 0);
+    for (int t = 0; t < 4; t++)
+        for (int i = 0; i < 256; i++) {
+            uint32_t g = T.zn(T.t[0][i], (uint64_t)gap + t);
+            for (int b = 0; b < 32; b++) img[g_dword_index(t, i, b)] = g;
+        }
+    for (int b = 0; b < 32; b++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[32768 + (size_t)(p * 16 + v) * 32 + b] = T.zinvn((uint32_t)v << (4 * p), 16u * (uint32_t)(b % lpb));
+    for (int u = 0; u < 3; u++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kV4UDword + (size_t)u * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 4u * (uint32_t)(u + 1));
+    for (int j = 0; j < 4; j++)
+        for (uint32_t v = 0; v < 256; v++) img[kG4UDword + 256 * j + v] = slice4_inv(v << (8 * j));
+    for (int i = 0; i < 256; i++) img[kG4T0Dword + i] = T.t[0][i];
+    return img;
 }
 
 // Small global-memory table used by the kernels' scalar epilogues:

@@ -122,4 +122,27 @@ __device__ __forceinline__ uint64_t sload64(const void *p) {
     return v;
 }
 
+// Uniform shift z^-d through 8 nibble tables at LDS byte `base` (16 dwords each).
+__device__ __forceinline__ uint32_t ushift(const uint32_t *lds, uint32_t c, uint32_t base) {
+    uint32_t a0 = lds_at(lds, base + 0 * 64 + ((c << 2) & 0x3cu));
+    uint32_t a1 = lds_at(lds, base + 1 * 64 + ((c >> 2) & 0x3cu));
+    uint32_t a2 = lds_at(lds, base + 2 * 64 + ((c >> 6) & 0x3cu));
+    uint32_t a3 = lds_at(lds, base + 3 * 64 + ((c >> 10) & 0x3cu));
+    uint32_t a4 = lds_at(lds, base + 4 * 64 + ((c >> 14) & 0x3cu));
+    uint32_t a5 = lds_at(lds, base + 5 * 64 + ((c >> 18) & 0x3cu));
+    uint32_t a6 = lds_at(lds, base + 6 * 64 + ((c >> 22) & 0x3cu));
+    uint32_t a7 = lds_at(lds, base + 7 * 64 + ((c >> 26) & 0x3cu));
+    return xor3(xor3(a0, a1, a2), xor3(a3, a4, a5), a6 ^ a7);
+}
+
+// XOR over each aligned group of LPB lanes (DPP, result in every lane of the group).
+template <int LPB>
+__device__ __forceinline__ uint32_t group_xor(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, true);  // quad_perm [2,3,0,1]
+    if (LPB >= 8) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, true);  // row_half_mirror
+    if (LPB >= 16) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, true);  // row_mirror
+    return v;
+}
+
 }  // namespace jlk

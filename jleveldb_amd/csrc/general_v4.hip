@@ -1,0 +1,519 @@
+// general_v4.hip — general-path engine on the v4 lane layout (variable block
+// lengths and alignment, per-block init/suffix, table/log verify epilogues).
+// Compiled once per mode (-DJL_MODE=k, Makefile); the mode-independent helper
+// kernels (keys, runs, round descriptors) live in the JL_MODE == 0 object.
+//
+// Work unit: a ROUND of up to 8 blocks with the same step count K, processed by
+// one wave exactly as the 4 KiB kernel (fixed_v4.hip) processes 8 blocks: 8
+// lanes per block, block-step 128 B, one 16-byte load per lane and step, 4
+// chains per lane through the gap tables z^(124+t)∘T0, the same epilogue.  A
+// block of n bytes is viewed END-aligned on the 128-B step grid: K = ceil(n/128)
+// steps, f = 128K - n virtual zero bytes in front, virtual start vs = p - f.
+// Rounds only hold blocks of one K (the host pipeline sorts blocks by K and
+// cuts every run of equal K into rounds of 8; fixed-stride batches need no
+// sort), so all 8 groups of a round run in lockstep and no block is padded.
+//
+// Seeding needs no state shift (as in the stream kernel): W = slice4^-1(~init)
+// is fed as the 4 data bytes just before the block, i.e. at virtual bytes
+// [f-4, f); when f < 4 its low bytes fall in virtual dword -4, the chain
+// (lane 7, dword 3) of step -1, which then starts from gstep(W << 8f).
+//
+// Step 0 holds the f pad bytes, so its lanes do not load their (unaligned,
+// possibly page-straddling) 16 bytes directly: every lane loads the two ALIGNED
+// 16-B chunks around its bytes (an aligned chunk that overlaps the block never
+// leaves the block's pages; a chunk that does not overlap it is replaced by the
+// chunk holding byte p), and assembles its 4 virtual dwords with v_alignbyte.
+// Steps k >= 1 lie inside [p, p+n) and load directly (unaligned dwordx4).
+//
+// Entries of a round in the register ring (one wave-wide load each):
+//   [side]  verify / init / suffix modes: lane 0 / 1 of each group load the
+//           aligned 16-B chunks holding the first / last byte of the stored crc
+//           (or holding init[i] / the suffix byte); other lanes load the zero page
+//   lo, hi  the two aligned chunks of step 0
+//   K-1     plain steps 1..K-1
+// The ring (P = 16 entries, s_waitcnt vmcnt(P-2) before each use, refill right
+// after) runs across rounds, so the HBM stream never drains.  Round
+// descriptors are read with scalar loads (lgkmcnt, never vmcnt).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdlib.h>
+
+#include "engine_device.hpp"
+
+#ifndef JL_MODE
+#error "compile with -DJL_MODE=<jlk::MODE_*>"
+#endif
+#ifndef JL_GV4_THREADS
+#define JL_GV4_THREADS 512  // 8 waves per CU: 256 VGPRs per lane for the ring + cursors
+#endif
+
+namespace jlk {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+// the 16 ring slots: (slot, register quad, its 4 registers)
+#define JL_GV4_SLOTS(X) \
+    X(0, "v[192:195]", "v192", "v193", "v194", "v195") \
+    X(1, "v[196:199]", "v196", "v197", "v198", "v199") \
+    X(2, "v[200:203]", "v200", "v201", "v202", "v203") \
+    X(3, "v[204:207]", "v204", "v205", "v206", "v207") \
+    X(4, "v[208:211]", "v208", "v209", "v210", "v211") \
+    X(5, "v[212:215]", "v212", "v213", "v214", "v215") \
+    X(6, "v[216:219]", "v216", "v217", "v218", "v219") \
+    X(7, "v[220:223]", "v220", "v221", "v222", "v223") \
+    X(8, "v[224:227]", "v224", "v225", "v226", "v227") \
+    X(9, "v[228:231]", "v228", "v229", "v230", "v231") \
+    X(10, "v[232:235]", "v232", "v233", "v234", "v235") \
+    X(11, "v[236:239]", "v236", "v237", "v238", "v239") \
+    X(12, "v[240:243]", "v240", "v241", "v242", "v243") \
+    X(13, "v[244:247]", "v244", "v245", "v246", "v247") \
+    X(14, "v[248:251]", "v248", "v249", "v250", "v251") \
+    X(15, "v[252:255]", "v252", "v253", "v254", "v255")
+
+template <int MODE>
+struct GV4 {
+    static constexpr bool VERIFY = MODE == MODE_TABLE_VERIFY || MODE == MODE_LOG_VERIFY;
+};
+
+// Per-lane view of a round's descriptor (group q = lane >> 3).
+struct RoundView {
+    uint64_t vs;   // per lane: the group's virtual start
+    uint32_t f;    // per lane
+    uint32_t idx;  // per lane (kGNull: no result)
+    uint32_t K;    // wave-uniform
+};
+
+__device__ __forceinline__ uint32_t sel8(uint32_t q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
+                                         uint32_t a5, uint32_t a6, uint32_t a7) {
+    const uint32_t lo = q & 4u ? (q & 2u ? (q & 1u ? a7 : a6) : (q & 1u ? a5 : a4))
+                               : (q & 2u ? (q & 1u ? a3 : a2) : (q & 1u ? a1 : a0));
+    return lo;
+}
+
+__device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, uint32_t q) {
+    RoundView v;
+    if (A.desc) {
+        // the round's 8 descriptors (128 B) with two scalar loads: SMEM/lgkmcnt, so the
+        // hand-counted vmcnt ring never sees them (a compiler-emitted vector load here
+        // would be waited for with vmcnt and drain the ring)
+        typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+        const uint64_t ga = uni64((uint64_t)(uintptr_t)(A.desc + r * 8u));
+        v16u d0, d1;
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                     : "=s"(d0), "=s"(d1) : "s"(ga) : "memory");
+        const uint32_t w[32] = {d0[0],  d0[1],  d0[2],  d0[3],  d0[4],  d0[5],  d0[6],  d0[7],
+                                d0[8],  d0[9],  d0[10], d0[11], d0[12], d0[13], d0[14], d0[15],
+                                d1[0],  d1[1],  d1[2],  d1[3],  d1[4],  d1[5],  d1[6],  d1[7],
+                                d1[8],  d1[9],  d1[10], d1[11], d1[12], d1[13], d1[14], d1[15]};
+        uint32_t vl[8], vh[8], ix[8], fs[8];
+        const uint32_t meta0 = w[3];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {  // GDesc i = {vs lo, vs hi, idx, meta} at dwords 4i..4i+3
+            ix[i] = w[4 * i + 2];
+            const bool nul = ix[i] == kGNull;
+            vl[i] = nul ? w[0] : w[4 * i];
+            vh[i] = nul ? w[1] : w[4 * i + 1];
+            fs[i] = (nul ? meta0 : w[4 * i + 3]) >> 25;
+        }
+        v.K = meta0 & 0x1ffffffu;  // one K per round
+        const uint32_t lo = sel8(q, vl[0], vl[1], vl[2], vl[3], vl[4], vl[5], vl[6], vl[7]);
+        const uint32_t hi = sel8(q, vh[0], vh[1], vh[2], vh[3], vh[4], vh[5], vh[6], vh[7]);
+        v.vs = ((uint64_t)hi << 32) | lo;
+        v.idx = sel8(q, ix[0], ix[1], ix[2], ix[3], ix[4], ix[5], ix[6], ix[7]);
+        v.f = sel8(q, fs[0], fs[1], fs[2], fs[3], fs[4], fs[5], fs[6], fs[7]);
+    } else {
+        const uint64_t i = uni64(r) * 8u + q;
+        const uint64_t ie = i < A.P.n ? i : uni64(r) * 8u;
+        v.K = A.fixed_K;
+        v.f = A.fixed_f;
+        v.vs = (uint64_t)(uintptr_t)A.P.base + ie * A.P.fixed_bytes - A.fixed_f;
+        v.idx = i < A.P.n ? (uint32_t)i : kGNull;
+    }
+    return v;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
+    const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
+    return K + 1u + (side ? 1u : 0u);
+}
+
+
+// Prefetch cursor: walks the wave's rounds r = w, w+W, ... entry by entry.
+template <int MODE>
+struct GPF {
+    uint64_t r, R, W;
+    uint32_t e, E, K;
+    uint64_t addr;        // per lane: next plain-step address
+    uint64_t lo, hi, side_addr;  // per lane: step-0 chunks and the side chunk
+    uint64_t dummy;           // a mapped address (zero page) for lanes with nothing to load
+
+    __device__ __forceinline__ void setup(const GV4Args &A, uint32_t lane) {
+        const uint32_t q = lane >> 3, l = lane & 7u;  // group, lane in group
+        RoundView v;
+        for (;;) {  // K == 0 rounds (empty blocks, results already written) are skipped
+            v = round_view(A, r, q);
+            if (uni(v.K) != 0u) break;
+            r = uni64(r + W);
+            if (r >= R) return;
+        }
+        K = uni(v.K);
+        E = uni(n_entries<MODE>(A, K));
+        const uint64_t p = v.vs + v.f, n = (uint64_t)K * 128u - v.f;
+        const uint64_t vstart = v.vs + 16u * l;
+        const uint64_t A16 = vstart & ~(uint64_t)15, pa = p & ~(uint64_t)15;
+        lo = (A16 + 16u > p) ? A16 : pa;
+        hi = (A16 + 32u > p && A16 + 16u < p + n) ? A16 + 16u : pa;
+        addr = vstart + 128u;
+        // side chunks (16-B aligned, each holding a byte of what is needed): lane 0 / 1 of the group
+        uint64_t c0 = pa, c1 = pa;
+        if (GV4<MODE>::VERIFY) {
+            const uint64_t sa = MODE == MODE_LOG_VERIFY ? p - 6u : p + n;  // stored crc
+            c0 = sa & ~(uint64_t)15;
+            c1 = (sa + 3u) & ~(uint64_t)15;
+        } else {
+            if (A.P.init && v.idx != kGNull) c0 = (uint64_t)(uintptr_t)(A.P.init + v.idx) & ~(uint64_t)15;
+            if (A.P.suffix && v.idx != kGNull) c1 = (uint64_t)(uintptr_t)(A.P.suffix + v.idx) & ~(uint64_t)15;
+        }
+        side_addr = l == 0u ? c0 : (l == 1u ? c1 : dummy);
+        e = 0;
+    }
+    __device__ __forceinline__ void init(const GV4Args &A, uint64_t w, uint64_t waves, uint64_t nr, uint32_t lane,
+                                         uint64_t dmy) {
+        r = w;
+        W = waves;
+        R = nr;
+        dummy = dmy;
+        if (r < R) setup(A, lane);
+    }
+    // Address of the next entry (advancing the cursor).  The ring load itself is
+    // issued by the caller at ONE site per slot: a load asm in several branches
+    // would give the slot's new value a phi at the join, and the register
+    // allocator may resolve that phi with a copy of the still-in-flight register.
+    __device__ __forceinline__ uint64_t next(const GV4Args &A, uint32_t lane) {
+        const uint64_t a = next_raw(A, lane);
+        if (A.P.dbg) {  // debugging (JL_GV4_DEBUG): log and neutralise loads outside the valid range
+            const uint64_t zp = dummy - 16u * lane;
+            if (!((a >= A.P.dbg_lo && a + 16 <= A.P.dbg_hi) || (a >= zp && a + 16 <= zp + 4096))) {
+                const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
+                if (slot < 256) {
+                    A.P.dbg[1 + 4 * slot] = r;
+                    A.P.dbg[2 + 4 * slot] = e;
+                    A.P.dbg[3 + 4 * slot] = lane;
+                    A.P.dbg[4 + 4 * slot] = a;
+                }
+                return dummy;
+            }
+        }
+        return a;
+    }
+    __device__ __forceinline__ uint64_t next_raw(const GV4Args &A, uint32_t lane) {
+        if (r >= R) return dummy;  // past the wave's last round: keep the ring count exact
+        const bool has_side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
+        const uint32_t e0 = has_side ? 1u : 0u;
+        uint64_t a;
+        if (e >= e0 + 2u) {
+            a = addr;
+            addr += 128u;
+        } else if (e == e0) {
+            a = lo;
+        } else if (e == e0 + 1u) {
+            a = hi;
+        } else {
+            a = side_addr;
+        }
+        if (++e == E) {
+            r += W;
+            if (r < R) setup(A, lane);
+            r = uni64(r);
+        }
+        e = uni(e);
+        return a;
+    }
+};
+
+template <int MODE, bool STRICT = false>
+__global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(192))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
+                                                       const uint8_t *__restrict__ zero) {
+    constexpr int P_ = 16;
+    __shared__ uint32_t lds[kImageBytes / 4];
+    load_image(lds, img);
+    const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
+    const GLanes gl(lane);
+    const uint32_t lc = 131072u | ((lane & 31u) << 2);
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t w = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint64_t R = A.desc ? (uint64_t)*A.n_rounds : (A.P.n + 7u) / 8u;
+    // compute cursor: the wave's first round with K > 0
+    uint64_t cr = w;
+    RoundView cv;
+    for (;;) {
+        if (cr >= R) return;
+        cv = round_view(A, cr, q);
+        if (uni(cv.K) != 0u) break;
+        cr = uni64(cr + waves);
+    }
+    const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
+    const uint32_t e0 = side ? 1u : 0u;
+    uint32_t zero_v;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
+
+    GPF<MODE> pf;
+    pf.init(A, cr, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
+    // The ring lives in PINNED registers v192..v255 (slot u = v[192+4u : 195+4u]),
+    // above the compiler's budget (amdgpu_num_vgpr(192)): the register allocator
+    // can never copy, reuse or spill a slot while its load is in flight — with
+    // compiler-allocated ring values this kernel's branchy rounds made it do that
+    // (r1: intermittent faults).  Each slot is touched only by inline asm: the
+    // load (which declares the slot clobbered), the wait, and the reads (the
+    // chains' final XOR takes the data word straight from the slot register).
+#define JL_LOAD(RQ, R0, R1, R2, R3)                                                                            \
+    {                                                                                                          \
+        const uint64_t a_ = pf.next(A, lane);                                                                  \
+        asm volatile("global_load_dwordx4 " RQ ", %0, off nt" ::"v"(a_) : "memory", R0, R1, R2, R3);           \
+    }
+#define JL_PRIME(u, RQ, R0, R1, R2, R3) JL_LOAD(RQ, R0, R1, R2, R3)
+    JL_GV4_SLOTS(JL_PRIME)
+#undef JL_PRIME
+
+    uint32_t cK = uni(cv.K), cE = uni(n_entries<MODE>(A, cK)), ce = 0;
+    v4u lo_c;
+    v4u side_c;  // lane 0 / 1 of each group: the side chunk
+    uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
+
+    // rare entries of a round: the side chunk, the two step-0 chunks
+    auto rare = [&](v4u wv) {
+        if (ce == e0) {
+            lo_c = wv;
+        } else if (ce == e0 + 1u) {
+            // ---- step 0: assemble the lane's 4 virtual dwords from the aligned chunks
+            const uint32_t f = cv.f;
+            const uint64_t vstart = cv.vs + 16u * l;
+            const uint32_t o = (uint32_t)(vstart & 15u), a = o >> 2, b = o & 3u;
+            // chunk data is garbage where it was replaced (those bytes are pad)
+            const uint32_t D0 = lo_c.x, D1 = lo_c.y, D2 = lo_c.z, D3 = lo_c.w, D4 = wv.x, D5 = wv.y, D6 = wv.z,
+                           D7 = wv.w;
+            auto pick = [&](uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+                return a & 2u ? (a & 1u ? m3 : m2) : (a & 1u ? m1 : m0);
+            };
+            const uint32_t E0 = pick(D0, D1, D2, D3), E1 = pick(D1, D2, D3, D4), E2 = pick(D2, D3, D4, D5),
+                           E3 = pick(D3, D4, D5, D6), E4 = pick(D4, D5, D6, D7);
+            uint32_t v[4] = {__builtin_amdgcn_alignbyte(E1, E0, b), __builtin_amdgcn_alignbyte(E2, E1, b),
+                             __builtin_amdgcn_alignbyte(E3, E2, b), __builtin_amdgcn_alignbyte(E4, E3, b)};
+            // seed word of this block
+            uint32_t W = A.seed0;
+            if (!GV4<MODE>::VERIFY && A.P.init) {
+                // init[idx] from lane 0's side chunk, broadcast to the group's 8 lanes
+                const uint64_t ia = (uint64_t)(uintptr_t)(A.P.init + (cv.idx == kGNull ? 0u : cv.idx));
+                const uint32_t k = (uint32_t)(ia >> 2) & 3u;
+                const uint32_t own = k & 2u ? (k & 1u ? side_c.w : side_c.z) : (k & 1u ? side_c.y : side_c.x);
+                const uint32_t y = ~(uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & ~7u) << 2), (int)own);
+                W = lds_at(lds, kG4UByte + ((y & 0xffu) << 2)) ^ lds_at(lds, kG4UByte + 1024u + (((y >> 8) & 0xffu) << 2)) ^
+                    lds_at(lds, kG4UByte + 2048u + (((y >> 16) & 0xffu) << 2)) ^
+                    lds_at(lds, kG4UByte + 3072u + ((y >> 24) << 2));
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int t = (int)(16u * l + 4u * j) - (int)f;  // dword start relative to p
+                const uint32_t dmask = t >= 0 ? 0xffffffffu : (t <= -4 ? 0u : 0xffffffffu << (8 * (-t)));
+                const int u = t + 4;  // relative to the seed's first byte
+                const uint32_t sp = (u >= 4 || u <= -4) ? 0u : (u >= 0 ? W >> (8 * u) : W << (8 * (-u)));
+                v[j] = (v[j] & dmask) | sp;
+            }
+            // virtual dword -4 (chain lane 7 / dword 3 of step -1) when f < 4
+            const uint32_t s73 = gstep(lds, f < 4u ? W << (8 * f) : 0u, gl);
+            const uint32_t i73 = (l == 7u && f < 4u) ? s73 : zero_v;
+            x0 = zero_v ^ v[0];
+            x1 = zero_v ^ v[1];
+            x2 = zero_v ^ v[2];
+            x3 = i73 ^ v[3];
+        } else {
+            side_c = wv;
+        }
+    };
+    // end of a round: epilogue, result, next round of the compute cursor; false when done
+    auto finish = [&]() -> bool {
+        const uint32_t s0 = gstep_x3(lds, x0, gl, 0u), s1 = gstep_x3(lds, x1, gl, 0u);
+        const uint32_t s2 = gstep_x3(lds, x2, gl, 0u), s3 = gstep_x3(lds, x3, gl, 0u);
+        const uint32_t c = xor3(s0, ushift(lds, s1, kV4U4Byte), ushift(lds, s2, kV4U4Byte + 512u)) ^
+                           ushift(lds, s3, kV4U4Byte + 1024u);
+        uint32_t st = group_xor<8>(realign(lds, c, lc));
+        // side chunks of lanes 0 and 1 of the group, seen from lane 0 (DPP row_shl:1)
+        const uint32_t h0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.x, 0x101, 0xf, 0xf, false);
+        const uint32_t h1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.y, 0x101, 0xf, 0xf, false);
+        const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.z, 0x101, 0xf, 0xf, false);
+        const uint32_t h3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.w, 0x101, 0xf, 0xf, false);
+        const uint64_t p = cv.vs + cv.f;
+        if (!GV4<MODE>::VERIFY && A.P.suffix) {
+            const uint64_t sa = (uint64_t)(uintptr_t)(A.P.suffix + (cv.idx == kGNull ? 0u : cv.idx));
+            const uint32_t k = (uint32_t)(sa >> 2) & 3u;
+            const uint32_t dw = k & 2u ? (k & 1u ? h3 : h2) : (k & 1u ? h1 : h0);
+            const uint32_t sfx = (dw >> (8u * (uint32_t)(sa & 3u))) & 0xffu;
+            st = (st >> 8) ^ lds_at(lds, kG4T0Byte + (((st ^ sfx) & 0xffu) << 2));
+        }
+        const uint32_t crc = ~st, m = mask_crc(crc);
+        if (A.P.dbg && l == 0u && cv.idx != kGNull && cv.idx >= A.P.n) {
+            const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
+            if (slot < 256) {
+                A.P.dbg[1 + 4 * slot] = cr;
+                A.P.dbg[2 + 4 * slot] = 0xffff;
+                A.P.dbg[3 + 4 * slot] = lane;
+                A.P.dbg[4 + 4 * slot] = cv.idx;
+            }
+        } else if (l == 0u && cv.idx != kGNull) {
+            if (MODE == MODE_CRC) {
+                A.P.out32[cv.idx] = (A.P.flags & 1u) ? m : crc;
+            } else {
+                const uint32_t n = cK * 128u - cv.f;
+                const uint64_t sa = MODE == MODE_LOG_VERIFY ? p - 6u : p + n;
+                // 32-B window: lane 0's chunk (sa & ~15) then lane 1's ((sa+3) & ~15, the same or the next)
+                const uint32_t o = (uint32_t)(sa & 15u), a = o >> 2, b = o & 3u;
+                const bool two = ((sa + 3u) & ~(uint64_t)15) != (sa & ~(uint64_t)15);
+                const uint32_t D0 = side_c.x, D1 = side_c.y, D2 = side_c.z, D3 = side_c.w;
+                const uint32_t D4 = two ? h0 : 0u;
+                const uint32_t lo_w = a & 2u ? (a & 1u ? D3 : D2) : (a & 1u ? D1 : D0);
+                const uint32_t hi_w = a & 2u ? (a & 1u ? D4 : D3) : (a & 1u ? D2 : D1);
+                const uint32_t stored = __builtin_amdgcn_alignbyte(hi_w, lo_w, b);
+                A.P.out8[cv.idx] = stored == m ? 1u : 0u;
+            }
+        }
+        // next round of the compute cursor (skipping K == 0 rounds)
+        for (;;) {
+            cr = uni64(cr + waves);
+            if (cr >= R) return false;
+            cv = round_view(A, cr, q);
+            if (uni(cv.K) != 0u) break;
+        }
+        cK = uni(cv.K);
+        cE = uni(n_entries<MODE>(A, cK));
+        ce = 0;
+        return true;
+    };
+
+    // plain step: the 4 lookups of each chain, then the XOR with the data word
+    // read straight from the slot register (one v_bitop3 per chain, as gstep_x3)
+#define JL_XS(x, R)                                                                                        \
+    {                                                                                                      \
+        const uint32_t a0_ = lds_at(lds, JL_GADDR(gl.l3, x, 0u)), a1_ = lds_at(lds, JL_GADDR(gl.l2, x, 1u));   \
+        const uint32_t a2_ = lds_at(lds, JL_GADDR(gl.l1, x, 2u)), a3_ = lds_at(lds, JL_GADDR(gl.l0, x, 3u));   \
+        const uint32_t t_ = xor3(a0_, a1_, a2_);                                                           \
+        asm volatile("v_bitop3_b32 %0, %1, %2, " R " bitop3:0x96" : "=v"(x) : "v"(t_), "v"(a3_));          \
+    }
+#define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
+    {                                                                                                      \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STRICT ? 0 : P_ - 2) : "memory");                         \
+        if (ce >= e0 + 2u) {                                                                               \
+            JL_XS(x0, R0) JL_XS(x1, R1) JL_XS(x2, R2) JL_XS(x3, R3)                                        \
+        } else {                                                                                           \
+            v4u wv_;                                                                                       \
+            uint32_t w0_, w1_, w2_, w3_;                                                                   \
+            asm volatile("v_mov_b32 %0, " R0 "\n\tv_mov_b32 %1, " R1 "\n\tv_mov_b32 %2, " R2                   \
+                         "\n\tv_mov_b32 %3, " R3                                                            \
+                         : "=v"(w0_), "=v"(w1_), "=v"(w2_), "=v"(w3_));                                     \
+            wv_.x = w0_;                                                                                   \
+            wv_.y = w1_;                                                                                   \
+            wv_.z = w2_;                                                                                   \
+            wv_.w = w3_;                                                                                   \
+            rare(wv_);                                                                                     \
+        }                                                                                                  \
+        if (++ce == cE && !finish()) break;                                                                \
+        JL_LOAD(RQ, R0, R1, R2, R3)                                                                        \
+    }
+    for (;;) {
+        JL_GV4_SLOTS(JL_G)
+    }
+#undef JL_G
+#undef JL_XS
+#undef JL_LOAD
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring drains before the wave ends
+}
+
+}  // namespace jlk
+
+namespace jlk {
+
+template <>
+hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
+    if (getenv("JL_GV4_STRICT"))  // debugging: vmcnt(0) before every ring use
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, true>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+                           zero);
+    else
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A, zero);
+    return hipGetLastError();
+}
+
+#if JL_MODE == 0
+// ---------------------------------------------------------------------------
+// Sorted pipeline: blocks -> (K, index) -> radix sort by K (host: hipcub) ->
+// run starts (max-scan of head positions) -> round heads every 8 blocks of a
+// run (sum-scan) -> GDesc table.  Blocks of K == 0 get their result here and
+// form K == 0 rounds that the main kernel skips.
+// ---------------------------------------------------------------------------
+__global__ void gv4_keys_kernel(KParams P, uint32_t *keys, uint32_t *vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const uint32_t n = P.len[i] + P.len_add;
+    const uint32_t K = (uint32_t)(((uint64_t)n + 127u) >> 7);
+    keys[i] = K < kGSoloKey ? K : kGSoloKey;
+    vals[i] = (uint32_t)i;
+    if (n == 0u) {  // extend(init, empty) = init (then the suffix byte)
+        uint32_t st = ~(P.init ? P.init[i] : 0u);
+        if (P.suffix) st = (st >> 8) ^ P.aux[(st ^ P.suffix[i]) & 0xffu];
+        const uint32_t crc = ~st;
+        if (P.mode == MODE_CRC) P.out32[i] = (P.flags & 1u) ? mask_crc(crc) : crc;
+        else P.out8[i] = 1u;
+    }
+}
+
+__global__ void gv4_heads_kernel(const uint32_t *sk, uint64_t n, uint32_t *h) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    h[j] = (j == 0 || sk[j] != sk[j - 1] || sk[j] == kGSoloKey) ? (uint32_t)j : 0u;
+}
+
+__global__ void gv4_rhead_kernel(const uint32_t *rs, uint64_t n, uint32_t *rh) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    rh[j] = ((j - rs[j]) & 7u) == 0 ? 1u : 0u;
+}
+
+__global__ void gv4_desc_kernel(KParams P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
+                                const uint32_t *rid, GDesc *desc, uint32_t *n_rounds) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n) return;
+    const uint32_t i = sv[j];
+    const uint32_t n = P.len[i] + P.len_add;
+    const uint32_t K = (uint32_t)(((uint64_t)n + 127u) >> 7);
+    const uint32_t f = (uint32_t)((uint64_t)K * 128u - n);
+    GDesc d;
+    d.vs = (uint64_t)(uintptr_t)P.base + P.off[i] - f;
+    d.idx = i;
+    d.meta = K | (f << 25);
+    desc[(uint64_t)(rid[j] - 1u) * 8u + ((j - rs[j]) & 7u)] = d;
+    if (j == P.n - 1) *n_rounds = rid[j];
+    (void)sk;
+}
+
+static inline dim3 grid1d(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+hipError_t launch_gv4_keys(const KParams &P, uint32_t *keys, uint32_t *vals, hipStream_t st) {
+    hipLaunchKernelGGL(gv4_keys_kernel, grid1d(P.n), dim3(256), 0, st, P, keys, vals);
+    return hipGetLastError();
+}
+hipError_t launch_gv4_heads(const uint32_t *sk, uint64_t n, uint32_t *h, hipStream_t st) {
+    hipLaunchKernelGGL(gv4_heads_kernel, grid1d(n), dim3(256), 0, st, sk, n, h);
+    return hipGetLastError();
+}
+hipError_t launch_gv4_rhead(const uint32_t *rs, uint64_t n, uint32_t *rh, hipStream_t st) {
+    hipLaunchKernelGGL(gv4_rhead_kernel, grid1d(n), dim3(256), 0, st, rs, n, rh);
+    return hipGetLastError();
+}
+hipError_t launch_gv4_desc(const KParams &P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
+                           const uint32_t *rid, GDesc *desc, uint32_t *n_rounds, hipStream_t st) {
+    hipLaunchKernelGGL(gv4_desc_kernel, grid1d(P.n), dim3(256), 0, st, P, sk, sv, rs, rid, desc, n_rounds);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace jlk

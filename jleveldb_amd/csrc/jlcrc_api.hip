@@ -172,6 +172,98 @@ static void free_partition(const jlk::KParams &P, uint64_t *part, hipStream_t st
     if (part) (void)hipFreeAsync((char *)part - ((P.n * 8 + 255) & ~(size_t)255), st);
 }
 
+// General v4 path (general_v4.hip): fixed strides run as implicit rounds; an
+// offset/length batch is sorted by step count K first (keys -> radix sort ->
+// run starts -> round ids -> GDesc table), all stream-ordered on `st` with
+// stream-ordered scratch.
+static bool gv4_eligible(const jlk::KParams &P) {
+    if (P.mode != jlk::MODE_CRC && P.mode != jlk::MODE_TABLE_VERIFY && P.mode != jlk::MODE_LOG_VERIFY) return false;
+    if (P.n >= (1ull << 31)) return false;  // hipcub sizes are int
+    if (!P.off && (P.fixed_bytes == 0 || P.fixed_bytes > 0xffffffffull)) return false;
+    return true;
+}
+
+static hipError_t gv4_launch(const jlk::GV4Args &A, hipStream_t st) {
+    const void *img = ctx().d_img_v4[1];  // 8 lanes per block
+    const int grid = ctx().cus;            // one 512-thread workgroup per CU (the LDS image)
+    switch (A.P.mode) {
+    case jlk::MODE_CRC: return jlk::launch_gv4_m<jlk::MODE_CRC>(img, A, ctx().d_zero, grid, st);
+    case jlk::MODE_TABLE_VERIFY: return jlk::launch_gv4_m<jlk::MODE_TABLE_VERIFY>(img, A, ctx().d_zero, grid, st);
+    default: return jlk::launch_gv4_m<jlk::MODE_LOG_VERIFY>(img, A, ctx().d_zero, grid, st);
+    }
+}
+
+static int run_gv4(const jlk::KParams &P, hipStream_t st) {
+    jlk::GV4Args A;
+    memset(&A, 0, sizeof(A));
+    A.P = P;
+    A.seed0 = jlmath::slice4_inv(0xffffffffu);
+    if (!P.off) {
+        const uint64_t fb = P.fixed_bytes;
+        A.fixed_K = (uint32_t)((fb + 127) / 128);
+        A.fixed_f = (uint32_t)((uint64_t)A.fixed_K * 128 - fb);
+        JL_HIP(gv4_launch(A, st));
+        return JL_OK;
+    }
+    const uint64_t n = P.n;
+    // rounds: one per 8 blocks of a run, runs <= distinct K (< 2^17) + solo blocks (>= 16 MiB each)
+    const uint64_t max_rounds = (n + 7) / 8 + (1ull << 17) + 18432 + 1;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    size_t t_sort = 0, t_max = 0, t_sum = 0;
+    uint32_t *nul = nullptr;
+    JL_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, nul, nul, nul, nul, (int)n, 0, 17, st));
+    JL_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, t_max, nul, nul, hipcub::Max(), (int)n, st));
+    JL_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, t_sum, nul, nul, (int)n, st));
+    const size_t tmp = std::max(t_sort, std::max(t_max, t_sum));
+    const size_t a4 = al(n * 4), ad = al(max_rounds * sizeof(jlk::GDesc) * 8);
+    const size_t total = 6 * a4 + ad + 256 + al(tmp);
+    char *buf = nullptr;
+    if (hipMallocAsync((void **)&buf, total, st) != hipSuccess) return fail(JL_ERR_NOMEM, "gv4 scratch allocation failed");
+    uint32_t *keys = (uint32_t *)buf, *vals = (uint32_t *)(buf + a4), *sk = (uint32_t *)(buf + 2 * a4),
+             *sv = (uint32_t *)(buf + 3 * a4), *rs = (uint32_t *)(buf + 4 * a4), *rid = (uint32_t *)(buf + 5 * a4);
+    jlk::GDesc *desc = (jlk::GDesc *)(buf + 6 * a4);
+    uint32_t *n_rounds = (uint32_t *)(buf + 6 * a4 + ad);
+    void *t = buf + 6 * a4 + ad + 256;
+    hipError_t e = hipSuccess;
+    size_t ts = tmp;
+    if (e == hipSuccess) e = hipMemsetAsync(desc, 0xff, max_rounds * sizeof(jlk::GDesc) * 8, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_keys(P, keys, vals, st);
+    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(t, ts, keys, sk, vals, sv, (int)n, 0, 17, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_heads(sk, n, keys, st);  // keys <- head positions
+    ts = tmp;
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveScan(t, ts, keys, rs, hipcub::Max(), (int)n, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_rhead(rs, n, vals, st);  // vals <- round-head flags
+    ts = tmp;
+    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(t, ts, vals, rid, (int)n, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_desc(P, sk, sv, rs, rid, desc, n_rounds, st);
+    A.desc = desc;
+    A.n_rounds = n_rounds;
+    unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
+    if (const char *dbg = getenv("JL_GV4_DEBUG")) {  // "lo:hi" valid load range (hex), debugging only
+        A.P.dbg_lo = strtoull(dbg, nullptr, 16);
+        const char *c = strchr(dbg, ':');
+        A.P.dbg_hi = c ? strtoull(c + 1, nullptr, 16) : ~0ull;
+        if (e == hipSuccess) e = hipMalloc((void **)&d_dbg, sizeof(h_dbg));
+        if (e == hipSuccess) e = hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st);
+        A.P.dbg = d_dbg;
+    }
+    if (e == hipSuccess) e = gv4_launch(A, st);
+    if (d_dbg) {
+        uint32_t hr = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&hr, n_rounds, 4, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipFree(d_dbg);
+        fprintf(stderr, "JL_GV4_DEBUG mode=%d n=%llu rounds=%u bad=%llu\n", P.mode, (unsigned long long)P.n, hr, h_dbg[0]);
+        for (unsigned long long i = 0; i < h_dbg[0] && i < 256; i++)
+            fprintf(stderr, "  round %llu entry %llu lane %llu addr/idx %llx\n", h_dbg[1 + 4 * i], h_dbg[2 + 4 * i],
+                    h_dbg[3 + 4 * i], h_dbg[4 + 4 * i]);
+    }
+    (void)hipFreeAsync(buf, st);
+    JL_HIP(e);
+    return JL_OK;
+}
+
 int run_general(const jlk::KParams &P, hipStream_t st) {
     if (P.n == 0) return JL_OK;
     // A/B knobs (tuning only; defaults are the measured best): JL_GENERAL=chunk
@@ -179,6 +271,7 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
     // depth (16/32/48), JL_NO_PARTITION the count split instead of bytes
     const char *e_g = getenv("JL_GENERAL");
     const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 16;
+    if (e_g && !strcmp(e_g, "gv4") && gv4_eligible(P)) return run_gv4(P, st);
     if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {
         JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
         return JL_OK;

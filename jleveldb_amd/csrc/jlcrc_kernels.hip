@@ -711,15 +711,12 @@ hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *z
 #undef JL_A
         return hipGetLastError();
     }
-    if (nt) {
-        if (depth <= 1) JL_L(true, 1);
-        else if (depth == 2) JL_L(true, 2);
-        else JL_L(true, 3);
-    } else {
-        if (depth <= 1) JL_L(false, 1);
-        else if (depth == 2) JL_L(false, 2);
-        else JL_L(false, 3);
-    }
+    // one block ahead only: the deeper r1 variants (D = 2, 3) counted the group's
+    // result store as a younger vmcnt operation, which the ring checker
+    // (tools/asm_ring_check.py) cannot prove safe; they were never faster
+    (void)depth;
+    if (nt) JL_L(true, 1);
+    else JL_L(false, 1);
 #undef JL_L
     return hipGetLastError();
 }

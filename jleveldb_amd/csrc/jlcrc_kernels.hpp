@@ -10,6 +10,9 @@ constexpr uint32_t kImageBytes = 163840;  // must equal jlmath::kImageBytes
 // v4 image (fixed_v4.hip, crc_math.hpp build_lds_image_v4): region B offsets
 constexpr uint32_t kV4U4Byte = 147456;   // uniform z^-4, z^-8, z^-12 nibble tables (512 B each)
 constexpr uint32_t kV4SlotDword = 37248; // per-wave result slots (64 dwords per wave)
+constexpr uint32_t kG4UByte = 153088;    // general v4: U_j[v] = slice4^-1(v << 8j), 4 x 256 dwords (seed of an init)
+constexpr uint32_t kG4T0Byte = 157184;   // general v4: T0 (suffix byte step)
+constexpr uint32_t kGNull = 0xffffffffu; // general v4: empty group of a round
 
 enum : int {
     MODE_CRC = 0,           // out32[i] = crc / mask(crc)
@@ -42,6 +45,22 @@ struct KParams {
     unsigned long long *dbg;
 };
 
+// general v4 path (general_v4.hip): group descriptor of the sorted pipeline
+// (16 B; 8 per round) and the kernel arguments
+struct GDesc {
+    uint64_t vs;    // virtual start p - f of the end-aligned view
+    uint32_t idx;   // block index (kGNull: empty group, mirrors group 0)
+    uint32_t meta;  // K | f << 25
+};
+struct GV4Args {
+    KParams P;
+    const GDesc *desc;          // null: implicit rounds of 8 consecutive fixed-stride blocks
+    const uint32_t *n_rounds;   // device count of rounds (sorted pipeline)
+    uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
+    uint32_t fixed_K, fixed_f;  // implicit rounds
+};
+constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
+
 struct LogEvent {  // layout-identical to jl_log_event
     uint64_t offset;
     uint32_t length;
@@ -57,6 +76,15 @@ hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *z
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
                              int grid, int lpb, int nt, hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
+// general v4 main kernel, one specialisation per mode (general_v4.hip -DJL_MODE=k; modes 0-2)
+template <int MODE>
+hipError_t launch_gv4_m(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st);
+// sorted-pipeline helpers (general_v4.hip, mode-0 object)
+hipError_t launch_gv4_keys(const KParams &P, uint32_t *keys, uint32_t *vals, hipStream_t st);
+hipError_t launch_gv4_heads(const uint32_t *sk, uint64_t n, uint32_t *h, hipStream_t st);
+hipError_t launch_gv4_rhead(const uint32_t *rs, uint64_t n, uint32_t *rh, hipStream_t st);
+hipError_t launch_gv4_desc(const KParams &P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
+                           const uint32_t *rid, GDesc *desc, uint32_t *n_rounds, hipStream_t st);
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
 template <int MODE>

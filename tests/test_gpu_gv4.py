@@ -1,0 +1,102 @@
+"""The general v4 kernel (general_v4.hip; JL_GENERAL=gv4 while it is being
+A/B'd) against the oracle: the variable-size, fixed-stride, table and log parity
+cases of test_gpu_parity.py re-run with it selected, plus cases aimed at its
+sorted-round pipeline (every K bucket, partial rounds, empty blocks mixed in,
+blocks around the 128-B step grid, a block above the solo threshold)."""
+import numpy as np
+import pytest
+
+import test_gpu_parity as base
+from test_gpu_parity import THREADS, to_dev, u32
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def gv4_kernel(monkeypatch):
+    monkeypatch.setenv("JL_GENERAL", "gv4")
+
+
+def test_gv4_every_length_and_alignment(gpu, jl, oracle):
+    base.test_batch_every_length_and_alignment(gpu, jl, oracle)
+
+
+def test_gv4_large_and_zipf(gpu, jl, oracle):
+    base.test_batch_large_and_zipf(gpu, jl, oracle)
+
+
+def test_gv4_golden_fixture(gpu, jl, golden):
+    base.test_batch_golden_fixture(gpu, jl, golden)
+
+
+@pytest.mark.parametrize("block_bytes", [1, 3, 4, 7, 64, 127, 128, 129, 255, 256, 1000, 1057, 4095, 4097, 65536, 100003])
+def test_gv4_fixed_other_sizes(gpu, jl, oracle, block_bytes):
+    base.test_fixed_other_sizes(gpu, jl, oracle, block_bytes)
+
+
+def test_gv4_step_grid_and_partial_rounds(gpu, jl, oracle):
+    """Lengths 128k-1..128k+1 for k up to 40, each repeated 1..9 times (partial
+    rounds of 8), interleaved with empty blocks, random order and alignment."""
+    rng = np.random.default_rng(21)
+    lens = []
+    for k in range(0, 41):
+        for d in (-1, 0, 1):
+            if 128 * k + d >= 0:
+                lens += [128 * k + d] * int(rng.integers(1, 10))
+    lens += [0] * 13
+    lens = np.array(lens, np.uint32)
+    rng.shuffle(lens)
+    gaps = rng.integers(0, 20, lens.size)
+    offs = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i in range(lens.size):
+        pos += int(gaps[i])
+        offs[i] = pos
+        pos += int(lens[i])
+    arena = rng.integers(0, 256, pos + 8, dtype=np.uint8)
+    d = (to_dev(arena, gpu), to_dev(offs.view(np.int64), gpu), to_dev(lens.view(np.int32), gpu))
+    assert np.array_equal(u32(jl.crc32c_batch_dev(*d)), oracle.batch(arena, offs, lens, threads=THREADS))
+    init = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    sfx = rng.integers(0, 256, lens.size, dtype=np.uint8)
+    got = u32(jl.crc32c_batch_dev(*d, init=to_dev(init.view(np.int32), gpu), suffix=to_dev(sfx, gpu), flags=0))
+    assert np.array_equal(got, oracle.batch(arena, offs, lens, init=init, suffix=sfx, flags=0, threads=THREADS))
+
+
+def test_gv4_block_at_allocation_edges(gpu, jl, oracle):
+    """First block at byte 0 of the allocation and the last ending at its last
+    byte (the step-0 chunks and stored-crc chunks must stay inside)."""
+    import torch
+
+    rng = np.random.default_rng(22)
+    for n in (1, 2, 5, 15, 16, 17, 127, 128, 129, 1000):
+        host = rng.integers(0, 256, n, dtype=np.uint8)
+        t = torch.from_numpy(host).to(gpu)
+        off = torch.zeros(1, dtype=torch.int64, device=gpu)
+        ln = torch.full((1,), n, dtype=torch.int32, device=gpu)
+        assert u32(jl.crc32c_batch_dev(t, off, ln))[0] == oracle.batch(host, np.zeros(1, np.uint64),
+                                                                      np.array([n], np.uint32))[0]
+
+
+def test_gv4_solo_block(gpu, jl, oracle):
+    """A block above the solo threshold (>= 131071 steps = 16 MiB) among small ones."""
+    rng = np.random.default_rng(23)
+    lens = np.array([5, (1 << 24) + 77, 300, 0, 129], np.uint32)
+    offs = np.zeros(lens.size, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = rng.integers(0, 256, int(lens.sum()) + 8, dtype=np.uint8)
+    got = u32(jl.crc32c_batch_dev(to_dev(arena, gpu), to_dev(offs.view(np.int64), gpu), to_dev(lens.view(np.int32), gpu)))
+    assert np.array_equal(got, oracle.batch(arena, offs, lens, threads=THREADS))
+
+
+def test_gv4_table(gpu, jl, oracle, golden):
+    base.test_table_trailers_and_verify(gpu, jl, oracle, golden)
+    base.test_table_many_blocks(gpu, jl, oracle)
+
+
+def test_gv4_log(gpu, jl, oracle, golden):
+    base.test_log_golden(gpu, jl, oracle, golden)
+    for seed in (3, 4):
+        base.test_log_random_with_corruption(gpu, jl, oracle, seed)
+    base.test_log_special_records(gpu, jl, oracle)
+    base.test_log_corruption_recovery(gpu, jl, oracle)
+    base.test_log_dev_resident(gpu, jl, oracle)

@@ -17,7 +17,7 @@ torch.cuda.set_device(0)
 jl.init(0)
 dev = torch.device("cuda:0")
 rounds = int(os.environ.get("ROUNDS", 3))
-variants = os.environ.get("VARIANTS", "chunk s16np s16 s32").split()
+variants = os.environ.get("VARIANTS", "s16 gv4").split()
 
 # C3
 rng = np.random.default_rng(SEED)
@@ -56,9 +56,9 @@ out2 = torch.empty(n2, dtype=torch.int32, device=dev)
 
 
 def setv(v):
-    os.environ["JL_GENERAL"] = "chunk" if v == "chunk" else "stream"
+    os.environ["JL_GENERAL"] = v if v in ("chunk", "gv4") else "stream"
     os.environ.pop("JL_NO_PARTITION", None)
-    if v != "chunk":
+    if v not in ("chunk", "gv4"):
         os.environ["JL_STREAM_DEPTH"] = v[1:].replace("np", "")
         if v.endswith("np"):
             os.environ["JL_NO_PARTITION"] = "1"
