@@ -52,24 +52,18 @@ namespace jlk {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// the 16 ring slots: (slot, register quad, its 4 registers)
+// the 8 ring slots: (slot, register quad, its 4 registers), pinned in v224..v255
+#define JL_GV4_RING 8
+#define JL_GV4_VGPR_BUDGET 224
 #define JL_GV4_SLOTS(X) \
-    X(0, "v[192:195]", "v192", "v193", "v194", "v195") \
-    X(1, "v[196:199]", "v196", "v197", "v198", "v199") \
-    X(2, "v[200:203]", "v200", "v201", "v202", "v203") \
-    X(3, "v[204:207]", "v204", "v205", "v206", "v207") \
-    X(4, "v[208:211]", "v208", "v209", "v210", "v211") \
-    X(5, "v[212:215]", "v212", "v213", "v214", "v215") \
-    X(6, "v[216:219]", "v216", "v217", "v218", "v219") \
-    X(7, "v[220:223]", "v220", "v221", "v222", "v223") \
-    X(8, "v[224:227]", "v224", "v225", "v226", "v227") \
-    X(9, "v[228:231]", "v228", "v229", "v230", "v231") \
-    X(10, "v[232:235]", "v232", "v233", "v234", "v235") \
-    X(11, "v[236:239]", "v236", "v237", "v238", "v239") \
-    X(12, "v[240:243]", "v240", "v241", "v242", "v243") \
-    X(13, "v[244:247]", "v244", "v245", "v246", "v247") \
-    X(14, "v[248:251]", "v248", "v249", "v250", "v251") \
-    X(15, "v[252:255]", "v252", "v253", "v254", "v255")
+    X(0, "v[224:227]", "v224", "v225", "v226", "v227") \
+    X(1, "v[228:231]", "v228", "v229", "v230", "v231") \
+    X(2, "v[232:235]", "v232", "v233", "v234", "v235") \
+    X(3, "v[236:239]", "v236", "v237", "v238", "v239") \
+    X(4, "v[240:243]", "v240", "v241", "v242", "v243") \
+    X(5, "v[244:247]", "v244", "v245", "v246", "v247") \
+    X(6, "v[248:251]", "v248", "v249", "v250", "v251") \
+    X(7, "v[252:255]", "v252", "v253", "v254", "v255")
 
 template <int MODE>
 struct GV4 {
@@ -234,9 +228,9 @@ struct GPF {
 };
 
 template <int MODE, bool STRICT = false>
-__global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(192))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
+__global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_GV4_VGPR_BUDGET))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
-    constexpr int P_ = 16;
+    constexpr int P_ = JL_GV4_RING;
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
@@ -391,20 +385,29 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(192)
         return true;
     };
 
-    // plain step: the 4 lookups of each chain, then the XOR with the data word
-    // read straight from the slot register (one v_bitop3 per chain, as gstep_x3)
-#define JL_XS(x, R)                                                                                        \
+    // plain step: the 16 lookups of the 4 chains, then ONE asm with the 4 XORs
+    // that take the data words straight from the slot registers (a volatile asm
+    // orders memory operations around it, so one per chain would serialise the
+    // chains' LDS latencies)
+#define JL_LK(x, T, A3)                                                                                    \
+    const uint32_t T = xor3(lds_at(lds, JL_GADDR(gl.l3, x, 0u)), lds_at(lds, JL_GADDR(gl.l2, x, 1u)),      \
+                            lds_at(lds, JL_GADDR(gl.l1, x, 2u)));                                          \
+    const uint32_t A3 = lds_at(lds, JL_GADDR(gl.l0, x, 3u));
+#define JL_XS4(R0, R1, R2, R3)                                                                             \
     {                                                                                                      \
-        const uint32_t a0_ = lds_at(lds, JL_GADDR(gl.l3, x, 0u)), a1_ = lds_at(lds, JL_GADDR(gl.l2, x, 1u));   \
-        const uint32_t a2_ = lds_at(lds, JL_GADDR(gl.l1, x, 2u)), a3_ = lds_at(lds, JL_GADDR(gl.l0, x, 3u));   \
-        const uint32_t t_ = xor3(a0_, a1_, a2_);                                                           \
-        asm volatile("v_bitop3_b32 %0, %1, %2, " R " bitop3:0x96" : "=v"(x) : "v"(t_), "v"(a3_));          \
+        JL_LK(x0, t0_, u0_) JL_LK(x1, t1_, u1_) JL_LK(x2, t2_, u2_) JL_LK(x3, t3_, u3_)                    \
+        asm volatile("v_bitop3_b32 %0, %4, %5, " R0 " bitop3:0x96\n\t"                                   \
+                     "v_bitop3_b32 %1, %6, %7, " R1 " bitop3:0x96\n\t"                                    \
+                     "v_bitop3_b32 %2, %8, %9, " R2 " bitop3:0x96\n\t"                                    \
+                     "v_bitop3_b32 %3, %10, %11, " R3 " bitop3:0x96"                                       \
+                     : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)                                           \
+                     : "v"(t0_), "v"(u0_), "v"(t1_), "v"(u1_), "v"(t2_), "v"(u2_), "v"(t3_), "v"(u3_));    \
     }
 #define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STRICT ? 0 : P_ - 2) : "memory");                         \
         if (ce >= e0 + 2u) {                                                                               \
-            JL_XS(x0, R0) JL_XS(x1, R1) JL_XS(x2, R2) JL_XS(x3, R3)                                        \
+            JL_XS4(R0, R1, R2, R3)                                                                         \
         } else {                                                                                           \
             v4u wv_;                                                                                       \
             uint32_t w0_, w1_, w2_, w3_;                                                                   \
@@ -424,7 +427,8 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(192)
         JL_GV4_SLOTS(JL_G)
     }
 #undef JL_G
-#undef JL_XS
+#undef JL_XS4
+#undef JL_LK
 #undef JL_LOAD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring drains before the wave ends
 }

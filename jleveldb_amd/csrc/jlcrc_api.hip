@@ -271,7 +271,11 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
     // depth (16/32/48), JL_NO_PARTITION the count split instead of bytes
     const char *e_g = getenv("JL_GENERAL");
     const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 16;
-    if (e_g && !strcmp(e_g, "gv4") && gv4_eligible(P)) return run_gv4(P, st);
+    // general v4 (general_v4.hip): the default for the log verify (C5: 1.46x the
+    // stream kernel, r1 bench), opt-in for the other modes (JL_GENERAL=gv4; the
+    // stream kernel is faster on C3); JL_GENERAL=stream forces the stream kernel
+    const bool want_gv4 = e_g ? !strcmp(e_g, "gv4") : P.mode == jlk::MODE_LOG_VERIFY;
+    if (want_gv4 && gv4_eligible(P)) return run_gv4(P, st);
     if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {
         JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
         return JL_OK;

@@ -1,5 +1,5 @@
-"""The general v4 kernel (general_v4.hip; JL_GENERAL=gv4 while it is being
-A/B'd) against the oracle: the variable-size, fixed-stride, table and log parity
+"""The general v4 kernel (general_v4.hip; the default for the log verify,
+JL_GENERAL=gv4 selects it for every mode) against the oracle: the variable-size, fixed-stride, table and log parity
 cases of test_gpu_parity.py re-run with it selected, plus cases aimed at its
 sorted-round pipeline (every K bucket, partial rounds, empty blocks mixed in,
 blocks around the 128-B step grid, a block above the solo threshold)."""
@@ -100,3 +100,9 @@ def test_gv4_log(gpu, jl, oracle, golden):
     base.test_log_special_records(gpu, jl, oracle)
     base.test_log_corruption_recovery(gpu, jl, oracle)
     base.test_log_dev_resident(gpu, jl, oracle)
+
+
+def test_log_through_stream_kernel(gpu, jl, oracle, golden, monkeypatch):
+    """The log verify defaults to gv4; the stream kernel (JL_GENERAL=stream) stays covered."""
+    monkeypatch.setenv("JL_GENERAL", "stream")
+    test_gv4_log(gpu, jl, oracle, golden)

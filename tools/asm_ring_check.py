@@ -146,7 +146,7 @@ def check_local(body):
     return sorted(problems)
 
 
-def check_pinned(body, first=192, last=255):
+def check_pinned(body, first=224, last=255):
     """For kernels whose ring lives in PINNED registers v[first..last] above the
     compiler's budget (general_v4.hip): no compiler-generated instruction may
     touch them, i.e. every reference must sit inside an inline-asm region
