@@ -35,6 +35,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import jleveldb_amd as jl  # noqa: E402
+from jleveldb_amd import shard as shd  # noqa: E402
 
 SEED = 0x4A4C4442
 PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
@@ -221,9 +222,9 @@ def main():
     stream = torch.cuda.current_stream()
 
     n = args.blocks
+    sh = shd.weak_shard(rank, world, n)  # rank r holds blocks [r*n, (r+1)*n) of the C4 set
     data = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
-    # rank r holds blocks [r*n, (r+1)*n) of the C4 set, generated in place
-    jl.fill_random_dev(data, SEED, first_word=rank * n * 512)
+    jl.fill_random_dev(data, SEED, first_word=sh.first_word)  # generated in place
     out = torch.empty(n, dtype=torch.int32, device=dev)
     step = lambda: jl.crc32c_fixed_dev(data, 4096, n, out=out)  # noqa: E731
 
@@ -246,13 +247,16 @@ def main():
     wall = time.perf_counter() - t0
     per_launch = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
     kern_ms = sum(per_launch) / args.steps
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-
-    bytes_step = world * n * 4096
-    value = bytes_step * args.steps / wall / GIB
+    wall = shd.job_wall_time(wall, dev)  # max over ranks (no-op at N=1)
+    value = shd.aggregate_rate(n * 4096, world, wall, args.steps)
+    gather_ms = None
+    if world > 1:  # result all-gather: reported beside, not part of the checksum path
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        shd.gather_results(out, world)
+        torch.cuda.synchronize()
+        gather_ms = shd.job_wall_time(time.perf_counter() - t0, dev) * 1e3
     alg_launch = n * (4096 + 4)
     achieved = alg_launch / (kern_ms / 1e3) / 1e9
     result = None
@@ -275,6 +279,7 @@ def main():
             "data": "synthetic (device splitmix64, seed 0x4A4C4442; rank r = blocks [r*1M,(r+1)*1M) of the C4 set)",
             "config": {"workload": "C2: 1M x 4 KiB random blocks per GPU, masked CRC32C, device-resident",
                        "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
+            "result_allgather_ms": None if gather_ms is None else round(gather_ms, 3),
             "roofline": {
                 "bound": "hbm",
                 "kernel": "crc_fixed4k_v4_kernel<8 lanes/block, nt>",
