@@ -34,6 +34,7 @@ extern "C" {
 #define JL_ERR_HIP (-3)       /* HIP runtime error (message in jl_last_error)   */
 #define JL_ERR_NOMEM (-4)     /* device or pinned-host allocation failed         */
 #define JL_ERR_CAPACITY (-5)  /* caller's output array too small                 */
+#define JL_ERR_CORRUPT (-6)   /* input is not a well-formed sstable (message in jl_last_error) */
 
 /* flags for the batch entry points */
 #define JL_FLAG_MASK 1u /* store Crc32C.mask(crc) (the on-disk form), else the raw crc */
@@ -113,6 +114,30 @@ int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint3
  * else 0 ("block checksum mismatch"). */
 int jl_table_verify_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, uint64_t n,
                         uint8_t *d_status, void *stream);
+/* Block handles of a whole SSTable image (host, no device work): parses the
+ * footer (TableFormat.Footer.decodeFrom, J/table/TableFormat.java:126-146), the
+ * index block's entries (Block.decodeEntry, J/table/Block.java:312-342; values
+ * are BlockHandle varints, TableFormat.java:74-78) and the metaindex block's
+ * (Table.readMeta, J/table/Table.java:287-310).  Writes *n handles (data blocks in
+ * index order, then meta/filter blocks, the metaindex, the index) with
+ * kind[i] = JL_BLOCK_*; every handle is checked to lie, with its 5-byte trailer,
+ * inside the file.  The index and metaindex blocks are read as Table.open /
+ * readMeta read them with paranoidChecks (TableFormat.readBlock,
+ * TableFormat.java:195-258: trailer checksum, then type byte; the reference's
+ * Snappy is a stub so only kNoCompression blocks are readable): a bad index
+ * block fails the walk, a bad metaindex block only drops the meta handles.  The
+ * arrays feed jl_table_verify[_dev] for whole-table verification.
+ * JL_ERR_CORRUPT with the reference's message ("file is too short to be an
+ * sstable", "not an sstable (bad magic number)", "block checksum mismatch",
+ * "corrupted compressed block contents", "bad compress type N", "bad block
+ * contents", "bad entry in block", "truncated block read") on a malformed file;
+ * JL_ERR_CAPACITY (and *n set) when cap < *n.  kind may be NULL. */
+#define JL_BLOCK_DATA 0
+#define JL_BLOCK_INDEX 1
+#define JL_BLOCK_METAINDEX 2
+#define JL_BLOCK_META 3
+int jl_table_block_handles(const uint8_t *file, uint64_t file_bytes, uint64_t *off, uint32_t *size, uint8_t *kind,
+                           uint64_t cap, uint64_t *n);
 /* Host-memory form (file = mmap'd .ldb bytes); blocking. */
 int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *off, const uint32_t *size, uint64_t n,
                     uint8_t *status);

@@ -84,6 +84,7 @@ def lib() -> ctypes.CDLL:
         "jl_table_trailers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
         "jl_table_verify_dev": (i32, [vp, vp, vp, u64, vp, vp]),
         "jl_table_verify": (i32, [vp, u64, vp, vp, u64, vp]),
+        "jl_table_block_handles": (i32, [vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_verify_dev": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64), vp]),
         "jl_log_verify": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_read_records": (i32, [vp, u64, i32, u64, vp, u64, vp, u64, ctypes.POINTER(u64), vp, u64,
@@ -280,6 +281,38 @@ def table_verify(file, off, size) -> np.ndarray:
     _check(lib().jl_table_verify(f.ctypes.data, f.size, off.ctypes.data, size.ctypes.data, off.size, st.ctypes.data),
            "jl_table_verify")
     return st
+
+
+BLOCK_DATA, BLOCK_INDEX, BLOCK_METAINDEX, BLOCK_META = 0, 1, 2, 3
+
+
+def table_block_handles(file):
+    """Every block handle of an SSTable image (data blocks in index order, then the
+    meta/filter blocks, the metaindex, the index): (offset u64[], size u32[],
+    kind u8[]).  Host parse of the footer and index/metaindex blocks; raises
+    JLError with the reference's Status message on a malformed table."""
+    f = _host(file)
+    cap = 64
+    while True:
+        off = np.zeros(cap, dtype=np.uint64)
+        size = np.zeros(cap, dtype=np.uint32)
+        kind = np.zeros(cap, dtype=np.uint8)
+        n = ctypes.c_uint64(0)
+        rc = lib().jl_table_block_handles(f.ctypes.data if f.size else None, f.size, off.ctypes.data,
+                                          size.ctypes.data, kind.ctypes.data, cap, ctypes.byref(n))
+        if rc == -5 and n.value > cap:  # JL_ERR_CAPACITY: grow and retry
+            cap = int(n.value)
+            continue
+        _check(rc, "jl_table_block_handles")
+        return off[: n.value], size[: n.value], kind[: n.value]
+
+
+def table_verify_file(file) -> tuple:
+    """Whole-table verification from the file bytes: the block handles of the table,
+    then the batched TableFormat.readBlock checksum test over all of them.
+    Returns (status u8[] per handle, off, size, kind)."""
+    off, size, kind = table_block_handles(file)
+    return table_verify(file, off, size), off, size, kind
 
 
 def table_verify_dev(file, off, size, out=None, stream=None):

@@ -311,6 +311,9 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
 
 }  // namespace
 
+// host-side helpers in other translation units (table_walker.cpp) report through here
+void jl_set_error(const std::string &msg) { g_err = msg; }
+
 extern "C" {
 
 const char *jl_last_error(void) { return g_err.c_str(); }

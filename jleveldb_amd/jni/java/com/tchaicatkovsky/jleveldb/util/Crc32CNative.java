@@ -28,6 +28,14 @@ public final class Crc32CNative {
     /** TableFormat.readBlock checksum test for many handles of one mmap'd table. */
     public static native int tableVerify(ByteBuffer file, long[] offset, int[] size, byte[] status);
 
+    /**
+     * Block handles of a whole mmap'd table (footer, index, metaindex walk):
+     * data blocks in index order, meta blocks, metaindex, index.  Returns the
+     * handle count (greater than offset.length: grow the arrays and call again)
+     * or a negative error code with the Status text in lastError().
+     */
+    public static native long tableBlockHandles(ByteBuffer file, long[] offset, int[] size, byte[] kind);
+
     /** LogReader verification of a whole log image; returns the number of 16-byte events. */
     public static native long logVerify(ByteBuffer log, boolean checksum, ByteBuffer events);
 }

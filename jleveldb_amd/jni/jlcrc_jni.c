@@ -94,6 +94,31 @@ JNIEXPORT jint JNICALL JFN(tableVerify)(JNIEnv *env, jclass cls, jobject file, j
     return r;
 }
 
+/* Block handles of a whole .ldb image (direct ByteBuffer): data blocks in
+ * index order, meta blocks, metaindex, index (jl_table_block_handles).  Returns
+ * the handle count — larger than the arrays when they are too short (grow and
+ * call again) — or a negative error (JL_ERR_CORRUPT: message in lastError()). */
+JNIEXPORT jlong JNICALL JFN(tableBlockHandles)(JNIEnv *env, jclass cls, jobject file, jlongArray off,
+                                               jintArray size, jbyteArray kind) {
+    (void)cls;
+    uint8_t *f = (*env)->GetDirectBufferAddress(env, file);
+    jlong cap = (*env)->GetDirectBufferCapacity(env, file);
+    jsize n = (*env)->GetArrayLength(env, off);
+    if (!f || cap < 0 || (*env)->GetArrayLength(env, size) != n || (*env)->GetArrayLength(env, kind) != n) {
+        throw_(env, "java/lang/IllegalArgumentException", "tableBlockHandles arguments");
+        return JL_ERR_INVALID;
+    }
+    uint64_t got = 0;
+    jlong *o = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
+    jint *s = (*env)->GetPrimitiveArrayCritical(env, size, NULL);
+    jbyte *k = (*env)->GetPrimitiveArrayCritical(env, kind, NULL);
+    int r = jl_table_block_handles(f, (uint64_t)cap, (uint64_t *)o, (uint32_t *)s, (uint8_t *)k, (uint64_t)n, &got);
+    (*env)->ReleasePrimitiveArrayCritical(env, kind, k, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, size, s, 0);
+    (*env)->ReleasePrimitiveArrayCritical(env, off, o, 0);
+    return (r == JL_OK || r == JL_ERR_CAPACITY) ? (jlong)got : (jlong)r;
+}
+
 /* Batched LogReader verification of a whole .log / MANIFEST image (direct
  * ByteBuffer): fills events as 16-byte jl_log_event records into `events`
  * (a direct ByteBuffer); returns the event count or a negative error. */

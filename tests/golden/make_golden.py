@@ -22,6 +22,10 @@ What is pinned and where it comes from:
   mixed-size records, its physical-record events and readRecord output.
 * ``table.bin``/``table.json`` — blocks with 5-byte trailers
   (TableBuilder.writeRawBlock, TableBuilder.java:305-323).
+* ``sstable.bin``/``sstable.json`` — a whole table written by the
+  oracle/sstable.py restatement of TableBuilder (TestCorruption.build(100)
+  shape, plus a filter block) and every block handle the walker must find.
+  No JVM here: parity of the walker is pinned to the restated writer.
 """
 from __future__ import annotations
 
@@ -178,6 +182,23 @@ def main() -> None:
         f.write(tfile)
     with open(os.path.join(HERE, "table.json"), "w") as f:
         json.dump({"handles": handles, "trailers": [oracle.table_trailer(b, 0).hex() for b in tblocks]}, f)
+
+    # ---- a whole SSTable (oracle/sstable.py restatement of TableBuilder), shaped
+    # like TestCorruption.build(100): keys "%016d" + 8-byte internal-key tag,
+    # 1000-byte values (TestCorruption.java:68, 125-143, 574-584), 4 KiB blocks,
+    # plus a filter block behind the metaindex.  Handles = the walker's expected output.
+    from oracle import sstable
+
+    srng = np.random.default_rng(0x53535442)
+    pairs = [(b"%016d" % i + struct.pack("<Q", (i + 1) << 8 | 1), srng.integers(0, 256, 1000, dtype=np.uint8).tobytes())
+             for i in range(100)]
+    sst, sh = sstable.build_table(pairs, filter_block=srng.integers(0, 256, 300, dtype=np.uint8).tobytes())
+    assert sstable.walk(sst) == sh
+    with open(os.path.join(HERE, "sstable.bin"), "wb") as f:
+        f.write(sst)
+    with open(os.path.join(HERE, "sstable.json"), "w") as f:
+        json.dump({"handles": [list(h) for h in sh], "n_pairs": len(pairs),
+                   "sha256": hashlib.sha256(sst).hexdigest()}, f)
     print("golden fixtures written; reference table sha256", ref_sha)
 
 
