@@ -52,19 +52,19 @@ __device__ __forceinline__ v4i make_rsrc(uint64_t base, uint32_t nbytes) {
     return r;
 }
 
-template <int LPB>
+template <int LPB, int RING = 16>
 struct V4Geom {
     static constexpr int STEP = 16 * LPB;   // bytes of one block-step
     static constexpr int S = 4096 / STEP;   // steps per block
     static constexpr int R = 64 / LPB;      // blocks per round
-    static constexpr int P = 16;            // ring slots = prefetch distance in steps
+    static constexpr int P = RING;          // ring slots = prefetch distance in steps
     static_assert(S % P == 0 || P % S == 0, "ring must tile the round");
     static_assert(S >= P, "at least one ring of steps per round");
 };
 
-template <int LPB, bool NT>
+template <int LPB, bool NT, int RING>
 struct V4Wave {
-    using Gm = V4Geom<LPB>;
+    using Gm = V4Geom<LPB, RING>;
     const uint32_t *lds;
     GLanes gl;
     uint32_t voff, lc, s_init, zero;
@@ -129,11 +129,11 @@ struct V4Wave {
     }
 };
 
-template <int LPB, bool NT>
-__global__ __launch_bounds__(1024) void crc_fixed4k_v4_kernel(const uint4 *__restrict__ img,
-                                                              const uint8_t *__restrict__ data, uint64_t n_blocks,
-                                                              uint32_t flags, uint32_t *__restrict__ out) {
-    using Gm = V4Geom<LPB>;
+template <int LPB, bool NT, int RING = 16, int THREADS = 1024>
+__global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__restrict__ img,
+                                                                 const uint8_t *__restrict__ data, uint64_t n_blocks,
+                                                                 uint32_t flags, uint32_t *__restrict__ out) {
+    using Gm = V4Geom<LPB, RING>;
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(1024) void crc_fixed4k_v4_kernel(const uint4 *__res
     const uint64_t dbase = (uint64_t)(uintptr_t)data;
     const uint32_t do_mask = flags & 1u;
 
-    V4Wave<LPB, NT> W(lds, lane);
+    V4Wave<LPB, NT, RING> W(lds, lane);
     W.voff = (lane / LPB) * 4096u + (lane % LPB) * 16u;
     W.lc = 131072u | ((lane & 31u) << 2);
     W.s_init = (lane % LPB == 0) ? 0xffffffffu : 0u;
@@ -193,10 +193,19 @@ __global__ __launch_bounds__(1024) void crc_fixed4k_v4_kernel(const uint4 *__res
 }
 
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
-                             int grid, int lpb, int nt, hipStream_t st) {
+                             int grid, int lpb, int nt, int shape, hipStream_t st) {
 #define JL_V4(L, N)                                                                                                 \
     hipLaunchKernelGGL((crc_fixed4k_v4_kernel<L, N>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, \
                        n_blocks, flags, out)
+#define JL_V4S(R, T)                                                                                                \
+    hipLaunchKernelGGL((crc_fixed4k_v4_kernel<8, true, R, T>), dim3(grid), dim3(T), 0, st, (const uint4 *)img, \
+                       data, n_blocks, flags, out)
+    // occupancy / ring-depth study shapes (ring slots, threads per CU): 1 = (8, 512), 2 = (16, 512), 3 = (8, 1024)
+    if (shape == 1) JL_V4S(8, 512);
+    else if (shape == 2) JL_V4S(16, 512);
+    else if (shape == 3) JL_V4S(8, 1024);
+    if (shape) return hipGetLastError();
+#undef JL_V4S
     if (lpb == 8) {
         if (nt) JL_V4(8, true);
         else JL_V4(8, false);

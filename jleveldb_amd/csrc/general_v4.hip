@@ -227,7 +227,9 @@ struct GPF {
     }
 };
 
-template <int MODE, bool STRICT = false>
+// VAR: 0 = default (nt ring loads), 1 = strict (vmcnt(0) before every ring use:
+// debugging), 2 = ring loads without nt (cache-policy study)
+template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_GV4_VGPR_BUDGET))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
     constexpr int P_ = JL_GV4_RING;
@@ -262,10 +264,17 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     // (r1: intermittent faults).  Each slot is touched only by inline asm: the
     // load (which declares the slot clobbered), the wait, and the reads (the
     // chains' final XOR takes the data word straight from the slot register).
+#define JL_GLD(RQ, ADDR, OFF, R0, R1, R2, R3)                                                                  \
+    if constexpr (VAR == 2)                                                                                    \
+        asm volatile("global_load_dwordx4 " RQ ", %0, off offset:%1" ::"v"(ADDR), "n"(OFF)                     \
+                     : "memory", R0, R1, R2, R3);                                                              \
+    else                                                                                                       \
+        asm volatile("global_load_dwordx4 " RQ ", %0, off offset:%1 nt" ::"v"(ADDR), "n"(OFF)                  \
+                     : "memory", R0, R1, R2, R3);
 #define JL_LOAD(RQ, R0, R1, R2, R3)                                                                            \
     {                                                                                                          \
         const uint64_t a_ = pf.next(A, lane);                                                                  \
-        asm volatile("global_load_dwordx4 " RQ ", %0, off nt" ::"v"(a_) : "memory", R0, R1, R2, R3);           \
+        JL_GLD(RQ, a_, 0, R0, R1, R2, R3)                                                                      \
     }
 #define JL_PRIME(u, RQ, R0, R1, R2, R3) JL_LOAD(RQ, R0, R1, R2, R3)
     JL_GV4_SLOTS(JL_PRIME)
@@ -405,7 +414,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     }
 #define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(STRICT ? 0 : P_ - 2) : "memory");                         \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
         if (ce >= e0 + 2u) {                                                                               \
             JL_XS4(R0, R1, R2, R3)                                                                         \
         } else {                                                                                           \
@@ -423,13 +432,35 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         if (++ce == cE && !finish()) break;                                                                \
         JL_LOAD(RQ, R0, R1, R2, R3)                                                                        \
     }
+    // Fast turn: the next P entries of BOTH cursors are plain steps of their
+    // current rounds (no rare entry, no epilogue, no round switch), so the turn
+    // is straight-line code: wait, the 4 chains, and the refill at the cursor's
+    // address + 128 u — no per-step bookkeeping.  Any other turn takes the
+    // general per-step path below (it always ends back on slot 0).
+#define JL_F(u, RQ, R0, R1, R2, R3)                                                                        \
+    {                                                                                                      \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
+        JL_XS4(R0, R1, R2, R3)                                                                             \
+        JL_GLD(RQ, pf.addr, 128 * (u), R0, R1, R2, R3)                                                     \
+    }
+    const bool fast_ok = !A.P.dbg;
     for (;;) {
+        if (fast_ok && ce >= e0 + 2u && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 + 2u &&
+            pf.e + (uint32_t)P_ < pf.E) {
+            JL_GV4_SLOTS(JL_F)
+            ce = uni(ce + (uint32_t)P_);
+            pf.e = uni(pf.e + (uint32_t)P_);
+            pf.addr += 128u * P_;
+            continue;
+        }
         JL_GV4_SLOTS(JL_G)
     }
+#undef JL_F
 #undef JL_G
 #undef JL_XS4
 #undef JL_LK
 #undef JL_LOAD
+#undef JL_GLD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring drains before the wave ends
 }
 
@@ -440,7 +471,10 @@ namespace jlk {
 template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
     if (getenv("JL_GV4_STRICT"))  // debugging: vmcnt(0) before every ring use
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, true>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+                           zero);
+    else if (getenv("JL_GV4_NONT"))  // study: ring loads without the nt cache policy
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
                            zero);
     else
         hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A, zero);

@@ -72,9 +72,10 @@ struct LogEvent {  // layout-identical to jl_log_event
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st);
-// v4 fast path (fixed_v4.hip): lpb = lanes per block (8, 16); img = the v4 image for that lpb
+// v4 fast path (fixed_v4.hip): lpb = lanes per block (8, 16); img = the v4 image for that lpb;
+// shape 0 = the default (16 ring slots, 1024 threads), 1..3 = occupancy study shapes
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
-                             int grid, int lpb, int nt, hipStream_t st);
+                             int grid, int lpb, int nt, int shape, hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
 // general v4 main kernel, one specialisation per mode (general_v4.hip -DJL_MODE=k; modes 0-2)
 template <int MODE>

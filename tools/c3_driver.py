@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""C3 (1M mixed Zipf blocks, 1 B-64 KiB, one arena) through the general path,
+LAUNCHES times: a short driver for rocprofv3 PMC passes (JL_GENERAL picks the
+kernel: stream / gv4)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import jleveldb_amd as jl  # noqa: E402
+
+SEED = 0x4A4C4442
+torch.cuda.set_device(0)
+jl.init(0)
+dev = torch.device("cuda:0")
+rng = np.random.default_rng(SEED)
+n = 1 << 20
+ks = np.empty(0, dtype=np.int64)
+while ks.size < n:
+    k = rng.zipf(1.1, 2 * n)
+    ks = np.concatenate([ks, k[k <= 64]])
+lens = (1024 * (ks[:n] - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
+if os.environ.get("C3_ALIGN"):  # study: every block 16-B aligned (lengths kept)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(((lens[:-1].astype(np.uint64) + 15) // 16) * 16, dtype=np.uint64)
+    total = int(offs[-1] + lens[-1])
+else:
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+arena = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+jl.fill_random_dev(arena, SEED + 3)
+d_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+out = torch.empty(n, dtype=torch.int32, device=dev)
+L = int(os.environ.get("LAUNCHES", 5))
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(L + 1)]
+ev[0].record()
+for i in range(L):
+    jl.crc32c_batch_dev(arena, d_off, d_len, out=out)
+    ev[i + 1].record()
+torch.cuda.synchronize()
+t = [ev[i].elapsed_time(ev[i + 1]) for i in range(L)]
+print(os.environ.get("JL_GENERAL", "default"), "C3 bytes", int(lens.sum(dtype=np.uint64)), "ms", [round(x, 3) for x in t])
