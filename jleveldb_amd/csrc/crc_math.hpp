@@ -163,6 +163,7 @@ constexpr size_t kV4UDword = 36864;
 constexpr size_t kV4SlotDword = 37248;
 constexpr size_t kG4UDword = 38272;
 constexpr size_t kG4T0Dword = 39296;
+constexpr size_t kG4DDword = 39552;  // 7 x 128 dwords, ends at 40448 <= kImageDwords
 inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     const Tables &T = tables();
     const int gap = 16 * lpb - 4;
@@ -183,6 +184,10 @@ inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     for (int j = 0; j < 4; j++)
         for (uint32_t v = 0; v < 256; v++) img[kG4UDword + 256 * j + v] = slice4_inv(v << (8 * j));
     for (int i = 0; i < 256; i++) img[kG4T0Dword + i] = T.t[0][i];
+    for (int u = 0; u < 7; u++)  // z^-(2^u): removes a tail pad of d bytes bit by bit
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kG4DDword + (size_t)u * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 1ull << u);
     return img;
 }
 

@@ -6,32 +6,32 @@
 // Work unit: a ROUND of up to 8 blocks with the same step count K, processed by
 // one wave exactly as the 4 KiB kernel (fixed_v4.hip) processes 8 blocks: 8
 // lanes per block, block-step 128 B, one 16-byte load per lane and step, 4
-// chains per lane through the gap tables z^(124+t)∘T0, the same epilogue.  A
-// block of n bytes is viewed END-aligned on the 128-B step grid: K = ceil(n/128)
-// steps, f = 128K - n virtual zero bytes in front, virtual start vs = p - f.
-// Rounds only hold blocks of one K (the host pipeline sorts blocks by K and
-// cuts every run of equal K into rounds of 8; fixed-stride batches need no
-// sort), so all 8 groups of a round run in lockstep and no block is padded.
+// chains per lane through the gap tables z^(124+t)∘T0, the same epilogue.
+//
+// A block [p, p+n) is viewed on the 128-B-ALIGNED grid of its memory: step k
+// is the window [A + 128k, +128), A = p & ~127, K = ceil((f + n)/128) windows
+// with a front pad of f = p - A bytes and a tail pad of d = 128K - f - n.
+// Every ring load is then one aligned 16-B chunk and a group's step one whole
+// 128-B line (unaligned dwordx4 loads that straddle lines made the texture
+// addresser the bottleneck, r1 PMC: TA busy ~100 %).  A window that holds a
+// byte of the block never leaves the block's pages, so no load can fault.
+// Pad bytes are masked to zero in the first / last step; zeros in front are
+// free, the d zeros behind advance the state by z^d, which the epilogue undoes
+// with z^-(2^i) for the set bits i of d.  Rounds only hold blocks of one K
+// (the host pipeline sorts blocks by K and cuts every run of equal K into
+// rounds of 8; 128-B aligned fixed-stride batches need no sort).
 //
 // Seeding needs no state shift (as in the stream kernel): W = slice4^-1(~init)
 // is fed as the 4 data bytes just before the block, i.e. at virtual bytes
 // [f-4, f); when f < 4 its low bytes fall in virtual dword -4, the chain
 // (lane 7, dword 3) of step -1, which then starts from gstep(W << 8f).
 //
-// Step 0 holds the f pad bytes, so its lanes do not load their (unaligned,
-// possibly page-straddling) 16 bytes directly: every lane loads the two ALIGNED
-// 16-B chunks around its bytes (an aligned chunk that overlaps the block never
-// leaves the block's pages; a chunk that does not overlap it is replaced by the
-// chunk holding byte p), and assembles its 4 virtual dwords with v_alignbyte.
-// Steps k >= 1 lie inside [p, p+n) and load directly (unaligned dwordx4).
-//
 // Entries of a round in the register ring (one wave-wide load each):
 //   [side]  verify / init / suffix modes: lane 0 / 1 of each group load the
 //           aligned 16-B chunks holding the first / last byte of the stored crc
 //           (or holding init[i] / the suffix byte); other lanes load the zero page
-//   lo, hi  the two aligned chunks of step 0
-//   K-1     plain steps 1..K-1
-// The ring (P = 16 entries, s_waitcnt vmcnt(P-2) before each use, refill right
+//   K       steps 0..K-1 (0 and K-1 mask their pads)
+// The ring (P = 8 entries, s_waitcnt vmcnt(P-2) before each use, refill right
 // after) runs across rounds, so the HBM stream never drains.  Round
 // descriptors are read with scalar loads (lgkmcnt, never vmcnt).
 #include <hip/hip_runtime.h>
@@ -72,8 +72,8 @@ struct GV4 {
 
 // Per-lane view of a round's descriptor (group q = lane >> 3).
 struct RoundView {
-    uint64_t vs;   // per lane: the group's virtual start
-    uint32_t f;    // per lane
+    uint64_t p;    // per lane: the group's first byte
+    uint32_t d;    // per lane: tail pad
     uint32_t idx;  // per lane (kGNull: no result)
     uint32_t K;    // wave-uniform
 };
@@ -90,38 +90,39 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
     if (A.desc) {
         // the round's 8 descriptors (128 B) with two scalar loads: SMEM/lgkmcnt, so the
         // hand-counted vmcnt ring never sees them (a compiler-emitted vector load here
-        // would be waited for with vmcnt and drain the ring)
+        // would be waited for with vmcnt and drain the ring).  Outputs are early-clobber:
+        // the first load's destination must not overlap the address the second one
+        // reads (r1: s[16:31] <- [s[16:17]] then [s[16:17] + 64] read a returned
+        // descriptor word as the address when the wave was descheduled in between)
         typedef uint32_t v16u __attribute__((ext_vector_type(16)));
         const uint64_t ga = uni64((uint64_t)(uintptr_t)(A.desc + r * 8u));
         v16u d0, d1;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(d0), "=s"(d1) : "s"(ga) : "memory");
+                     : "=&s"(d0), "=&s"(d1) : "s"(ga) : "memory");
         const uint32_t w[32] = {d0[0],  d0[1],  d0[2],  d0[3],  d0[4],  d0[5],  d0[6],  d0[7],
                                 d0[8],  d0[9],  d0[10], d0[11], d0[12], d0[13], d0[14], d0[15],
                                 d1[0],  d1[1],  d1[2],  d1[3],  d1[4],  d1[5],  d1[6],  d1[7],
                                 d1[8],  d1[9],  d1[10], d1[11], d1[12], d1[13], d1[14], d1[15]};
-        uint32_t vl[8], vh[8], ix[8], fs[8];
-        const uint32_t meta0 = w[3];
+        uint32_t vl[8], vh[8], ix[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {  // GDesc i = {vs lo, vs hi, idx, meta} at dwords 4i..4i+3
+        for (int i = 0; i < 8; i++) {  // GDesc i = {pd lo, pd hi, idx, K} at dwords 4i..4i+3
             ix[i] = w[4 * i + 2];
             const bool nul = ix[i] == kGNull;
             vl[i] = nul ? w[0] : w[4 * i];
             vh[i] = nul ? w[1] : w[4 * i + 1];
-            fs[i] = (nul ? meta0 : w[4 * i + 3]) >> 25;
         }
-        v.K = meta0 & 0x1ffffffu;  // one K per round
+        v.K = w[3];  // one K per round
         const uint32_t lo = sel8(q, vl[0], vl[1], vl[2], vl[3], vl[4], vl[5], vl[6], vl[7]);
         const uint32_t hi = sel8(q, vh[0], vh[1], vh[2], vh[3], vh[4], vh[5], vh[6], vh[7]);
-        v.vs = ((uint64_t)hi << 32) | lo;
+        v.p = ((uint64_t)(hi & 0xffffffu) << 32) | lo;
+        v.d = hi >> 24;
         v.idx = sel8(q, ix[0], ix[1], ix[2], ix[3], ix[4], ix[5], ix[6], ix[7]);
-        v.f = sel8(q, fs[0], fs[1], fs[2], fs[3], fs[4], fs[5], fs[6], fs[7]);
-    } else {
+    } else {  // 128-B aligned base and stride (run_gv4): f = d = 0
         const uint64_t i = uni64(r) * 8u + q;
         const uint64_t ie = i < A.P.n ? i : uni64(r) * 8u;
         v.K = A.fixed_K;
-        v.f = A.fixed_f;
-        v.vs = (uint64_t)(uintptr_t)A.P.base + ie * A.P.fixed_bytes - A.fixed_f;
+        v.d = 0;
+        v.p = (uint64_t)(uintptr_t)A.P.base + ie * A.P.fixed_bytes;
         v.idx = i < A.P.n ? (uint32_t)i : kGNull;
     }
     return v;
@@ -130,7 +131,7 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
 template <int MODE>
 __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
     const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
-    return K + 1u + (side ? 1u : 0u);
+    return K + (side ? 1u : 0u);
 }
 
 
@@ -139,9 +140,9 @@ template <int MODE>
 struct GPF {
     uint64_t r, R, W;
     uint32_t e, E, K;
-    uint64_t addr;        // per lane: next plain-step address
-    uint64_t lo, hi, side_addr;  // per lane: step-0 chunks and the side chunk
-    uint64_t dummy;           // a mapped address (zero page) for lanes with nothing to load
+    uint64_t addr;        // per lane: next step's chunk address
+    uint64_t side_addr;   // per lane: the side chunk
+    uint64_t dummy;       // a mapped address (zero page) for lanes with nothing to load
 
     __device__ __forceinline__ void setup(const GV4Args &A, uint32_t lane) {
         const uint32_t q = lane >> 3, l = lane & 7u;  // group, lane in group
@@ -154,12 +155,9 @@ struct GPF {
         }
         K = uni(v.K);
         E = uni(n_entries<MODE>(A, K));
-        const uint64_t p = v.vs + v.f, n = (uint64_t)K * 128u - v.f;
-        const uint64_t vstart = v.vs + 16u * l;
-        const uint64_t A16 = vstart & ~(uint64_t)15, pa = p & ~(uint64_t)15;
-        lo = (A16 + 16u > p) ? A16 : pa;
-        hi = (A16 + 32u > p && A16 + 16u < p + n) ? A16 + 16u : pa;
-        addr = vstart + 128u;
+        const uint64_t p = v.p, n = (uint64_t)K * 128u - (p & 127u) - v.d;
+        const uint64_t pa = p & ~(uint64_t)15;
+        addr = (p & ~(uint64_t)127) + 16u * l;
         // side chunks (16-B aligned, each holding a byte of what is needed): lane 0 / 1 of the group
         uint64_t c0 = pa, c1 = pa;
         if (GV4<MODE>::VERIFY) {
@@ -207,13 +205,9 @@ struct GPF {
         const bool has_side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
         const uint32_t e0 = has_side ? 1u : 0u;
         uint64_t a;
-        if (e >= e0 + 2u) {
+        if (e >= e0) {
             a = addr;
             addr += 128u;
-        } else if (e == e0) {
-            a = lo;
-        } else if (e == e0 + 1u) {
-            a = hi;
         } else {
             a = side_addr;
         }
@@ -281,29 +275,28 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
 #undef JL_PRIME
 
     uint32_t cK = uni(cv.K), cE = uni(n_entries<MODE>(A, cK)), ce = 0;
-    v4u lo_c;
     v4u side_c;  // lane 0 / 1 of each group: the side chunk
     uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
 
-    // rare entries of a round: the side chunk, the two step-0 chunks
+    // rare entries of a round: the side chunk, step 0 (front pad, seed), step K-1 (tail pad)
     auto rare = [&](v4u wv) {
+        if (ce < e0) {
+            side_c = wv;
+            return;
+        }
+        const uint32_t f = (uint32_t)(cv.p & 127u);
+        uint32_t v[4] = {wv.x, wv.y, wv.z, wv.w};
+        if (ce + 1u == cE) {  // last step: zero the tail pad (bytes >= 128 - d of the window)
+            const uint32_t lim = 128u - cv.d;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t u = 16u * l + 4u * j;
+                const uint32_t m = u + 4u <= lim ? 0xffffffffu : (u >= lim ? 0u : 0xffffffffu >> (8u * (u + 4u - lim)));
+                v[j] &= m;
+            }
+        }
         if (ce == e0) {
-            lo_c = wv;
-        } else if (ce == e0 + 1u) {
-            // ---- step 0: assemble the lane's 4 virtual dwords from the aligned chunks
-            const uint32_t f = cv.f;
-            const uint64_t vstart = cv.vs + 16u * l;
-            const uint32_t o = (uint32_t)(vstart & 15u), a = o >> 2, b = o & 3u;
-            // chunk data is garbage where it was replaced (those bytes are pad)
-            const uint32_t D0 = lo_c.x, D1 = lo_c.y, D2 = lo_c.z, D3 = lo_c.w, D4 = wv.x, D5 = wv.y, D6 = wv.z,
-                           D7 = wv.w;
-            auto pick = [&](uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
-                return a & 2u ? (a & 1u ? m3 : m2) : (a & 1u ? m1 : m0);
-            };
-            const uint32_t E0 = pick(D0, D1, D2, D3), E1 = pick(D1, D2, D3, D4), E2 = pick(D2, D3, D4, D5),
-                           E3 = pick(D3, D4, D5, D6), E4 = pick(D4, D5, D6, D7);
-            uint32_t v[4] = {__builtin_amdgcn_alignbyte(E1, E0, b), __builtin_amdgcn_alignbyte(E2, E1, b),
-                             __builtin_amdgcn_alignbyte(E3, E2, b), __builtin_amdgcn_alignbyte(E4, E3, b)};
+            // ---- step 0: zero the front pad, feed the seed word W as the 4 bytes before p
             // seed word of this block
             uint32_t W = A.seed0;
             if (!GV4<MODE>::VERIFY && A.P.init) {
@@ -332,7 +325,10 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
             x2 = zero_v ^ v[2];
             x3 = i73 ^ v[3];
         } else {
-            side_c = wv;
+            x0 = gstep_x3(lds, x0, gl, v[0]);
+            x1 = gstep_x3(lds, x1, gl, v[1]);
+            x2 = gstep_x3(lds, x2, gl, v[2]);
+            x3 = gstep_x3(lds, x3, gl, v[3]);
         }
     };
     // end of a round: epilogue, result, next round of the compute cursor; false when done
@@ -342,12 +338,21 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         const uint32_t c = xor3(s0, ushift(lds, s1, kV4U4Byte), ushift(lds, s2, kV4U4Byte + 512u)) ^
                            ushift(lds, s3, kV4U4Byte + 1024u);
         uint32_t st = group_xor<8>(realign(lds, c, lc));
+        // undo the tail pad: st is the state after d zero bytes past the block
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const bool bit = (cv.d >> i) & 1u;
+            if (__builtin_amdgcn_ballot_w64(bit)) {
+                const uint32_t sh = ushift(lds, st, kG4DByte + 512u * i);
+                st = bit ? sh : st;
+            }
+        }
         // side chunks of lanes 0 and 1 of the group, seen from lane 0 (DPP row_shl:1)
         const uint32_t h0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.x, 0x101, 0xf, 0xf, false);
         const uint32_t h1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.y, 0x101, 0xf, 0xf, false);
         const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.z, 0x101, 0xf, 0xf, false);
         const uint32_t h3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.w, 0x101, 0xf, 0xf, false);
-        const uint64_t p = cv.vs + cv.f;
+        const uint64_t p = cv.p;
         if (!GV4<MODE>::VERIFY && A.P.suffix) {
             const uint64_t sa = (uint64_t)(uintptr_t)(A.P.suffix + (cv.idx == kGNull ? 0u : cv.idx));
             const uint32_t k = (uint32_t)(sa >> 2) & 3u;
@@ -368,7 +373,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
             if (MODE == MODE_CRC) {
                 A.P.out32[cv.idx] = (A.P.flags & 1u) ? m : crc;
             } else {
-                const uint32_t n = cK * 128u - cv.f;
+                const uint32_t n = cK * 128u - (uint32_t)(p & 127u) - cv.d;
                 const uint64_t sa = MODE == MODE_LOG_VERIFY ? p - 6u : p + n;
                 // 32-B window: lane 0's chunk (sa & ~15) then lane 1's ((sa+3) & ~15, the same or the next)
                 const uint32_t o = (uint32_t)(sa & 15u), a = o >> 2, b = o & 3u;
@@ -415,7 +420,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
 #define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
-        if (ce >= e0 + 2u) {                                                                               \
+        if (ce > e0 && ce + 1u < cE) {                                                                     \
             JL_XS4(R0, R1, R2, R3)                                                                         \
         } else {                                                                                           \
             v4u wv_;                                                                                       \
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     }
     const bool fast_ok = !A.P.dbg;
     for (;;) {
-        if (fast_ok && ce >= e0 + 2u && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 + 2u &&
+        if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
             pf.e + (uint32_t)P_ < pf.E) {
             JL_GV4_SLOTS(JL_F)
             ce = uni(ce + (uint32_t)P_);
@@ -488,11 +493,30 @@ hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_
 // run (sum-scan) -> GDesc table.  Blocks of K == 0 get their result here and
 // form K == 0 rounds that the main kernel skips.
 // ---------------------------------------------------------------------------
+// block i: its first byte and length (fixed-stride batches that are not 128-B
+// aligned come through here too, with P.off == null)
+__device__ __forceinline__ void gv4_block(const KParams &P, uint64_t i, uint64_t &p, uint32_t &n) {
+    if (P.off) {
+        p = (uint64_t)(uintptr_t)P.base + P.off[i];
+        n = P.len[i] + P.len_add;
+    } else {
+        p = (uint64_t)(uintptr_t)P.base + i * P.fixed_bytes;
+        n = (uint32_t)P.fixed_bytes;
+    }
+}
+
+// steps of block (p, n) on the 128-B aligned grid
+__device__ __forceinline__ uint32_t gv4_K(uint64_t p, uint32_t n) {
+    return n ? (uint32_t)(((p & 127u) + (uint64_t)n + 127u) >> 7) : 0u;
+}
+
 __global__ void gv4_keys_kernel(KParams P, uint32_t *keys, uint32_t *vals) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
-    const uint32_t n = P.len[i] + P.len_add;
-    const uint32_t K = (uint32_t)(((uint64_t)n + 127u) >> 7);
+    uint64_t p;
+    uint32_t n;
+    gv4_block(P, i, p, n);
+    const uint32_t K = gv4_K(p, n);
     keys[i] = K < kGSoloKey ? K : kGSoloKey;
     vals[i] = (uint32_t)i;
     if (n == 0u) {  // extend(init, empty) = init (then the suffix byte)
@@ -521,14 +545,16 @@ __global__ void gv4_desc_kernel(KParams P, const uint32_t *sk, const uint32_t *s
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= P.n) return;
     const uint32_t i = sv[j];
-    const uint32_t n = P.len[i] + P.len_add;
-    const uint32_t K = (uint32_t)(((uint64_t)n + 127u) >> 7);
-    const uint32_t f = (uint32_t)((uint64_t)K * 128u - n);
-    GDesc d;
-    d.vs = (uint64_t)(uintptr_t)P.base + P.off[i] - f;
-    d.idx = i;
-    d.meta = K | (f << 25);
-    desc[(uint64_t)(rid[j] - 1u) * 8u + ((j - rs[j]) & 7u)] = d;
+    uint64_t p;
+    uint32_t n;
+    gv4_block(P, i, p, n);
+    const uint32_t K = gv4_K(p, n);
+    const uint64_t d = K ? (uint64_t)K * 128u - (p & 127u) - n : 0u;  // tail pad, < 128
+    GDesc g;
+    g.pd = p | (d << 56);
+    g.idx = i;
+    g.K = K;
+    desc[(uint64_t)(rid[j] - 1u) * 8u + ((j - rs[j]) & 7u)] = g;
     if (j == P.n - 1) *n_rounds = rid[j];
     (void)sk;
 }

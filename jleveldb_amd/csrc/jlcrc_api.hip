@@ -172,8 +172,8 @@ static void free_partition(const jlk::KParams &P, uint64_t *part, hipStream_t st
     if (part) (void)hipFreeAsync((char *)part - ((P.n * 8 + 255) & ~(size_t)255), st);
 }
 
-// General v4 path (general_v4.hip): fixed strides run as implicit rounds; an
-// offset/length batch is sorted by step count K first (keys -> radix sort ->
+// General v4 path (general_v4.hip): 128-B aligned fixed strides run as implicit
+// rounds; any other batch is sorted by step count K first (keys -> radix sort ->
 // run starts -> round ids -> GDesc table), all stream-ordered on `st` with
 // stream-ordered scratch.
 static bool gv4_eligible(const jlk::KParams &P) {
@@ -198,10 +198,9 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     memset(&A, 0, sizeof(A));
     A.P = P;
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
-    if (!P.off) {
-        const uint64_t fb = P.fixed_bytes;
-        A.fixed_K = (uint32_t)((fb + 127) / 128);
-        A.fixed_f = (uint32_t)((uint64_t)A.fixed_K * 128 - fb);
+    if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0) {
+        // every block starts on the 128-B grid: implicit rounds, no pads, no sort
+        A.fixed_K = (uint32_t)(P.fixed_bytes / 128);
         JL_HIP(gv4_launch(A, st));
         return JL_OK;
     }

@@ -12,6 +12,7 @@ constexpr uint32_t kV4U4Byte = 147456;   // uniform z^-4, z^-8, z^-12 nibble tab
 constexpr uint32_t kV4SlotDword = 37248; // per-wave result slots (64 dwords per wave)
 constexpr uint32_t kG4UByte = 153088;    // general v4: U_j[v] = slice4^-1(v << 8j), 4 x 256 dwords (seed of an init)
 constexpr uint32_t kG4T0Byte = 157184;   // general v4: T0 (suffix byte step)
+constexpr uint32_t kG4DByte = 158208;    // general v4: z^-(2^i), i = 0..6, nibble tables (tail-pad removal)
 constexpr uint32_t kGNull = 0xffffffffu; // general v4: empty group of a round
 
 enum : int {
@@ -48,16 +49,16 @@ struct KParams {
 // general v4 path (general_v4.hip): group descriptor of the sorted pipeline
 // (16 B; 8 per round) and the kernel arguments
 struct GDesc {
-    uint64_t vs;    // virtual start p - f of the end-aligned view
+    uint64_t pd;    // first byte p (bits 0..55) | tail pad d << 56 of the 128-B-aligned grid
     uint32_t idx;   // block index (kGNull: empty group, mirrors group 0)
-    uint32_t meta;  // K | f << 25
+    uint32_t K;     // steps: the 128-B windows [p & ~127 + 128k, +128) that hold the block
 };
 struct GV4Args {
     KParams P;
     const GDesc *desc;          // null: implicit rounds of 8 consecutive fixed-stride blocks
     const uint32_t *n_rounds;   // device count of rounds (sorted pipeline)
     uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
-    uint32_t fixed_K, fixed_f;  // implicit rounds
+    uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
 };
 constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
 

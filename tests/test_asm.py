@@ -59,3 +59,41 @@ def test_no_stale_ring_reads(asm):
 
     problems = {s: one(s, b) for s, b in ks.items()}
     assert not {s: p[:3] for s, p in problems.items() if p}
+
+
+def _sgprs(tok):
+    import re
+
+    m = re.fullmatch(r"s\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"s(\d+)", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def test_no_smem_address_clobbered_inside_an_asm_block(asm):
+    """Inside one inline-asm block, a scalar load's destination must not overlap
+    the address SGPRs of a later scalar load of the same block: the first load's
+    data can land before the second one reads its address (r1: the round
+    descriptors' two s_load_dwordx16 shared s[16:17] / s[16:31]; a descheduled
+    wave then loaded from a descriptor word, an aperture-violation fault)."""
+    bad = []
+    block = None
+    for line in asm.split("\n"):
+        if ";;#ASMSTART" in line:
+            block = []
+            continue
+        if ";;#ASMEND" in line:
+            block = None
+            continue
+        if block is None:
+            continue
+        ins = line.split(";")[0].strip()
+        if not ins.startswith("s_load") and not ins.startswith("s_buffer_load"):
+            continue
+        ops = [o.strip() for o in ins.split(None, 1)[1].split(",")]
+        dst, addr = _sgprs(ops[0]), _sgprs(ops[1])
+        if any(addr & d for d in block):
+            bad.append(ins)
+        block.append(dst)
+    assert not bad, bad[:5]

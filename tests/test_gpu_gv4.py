@@ -106,3 +106,16 @@ def test_log_through_stream_kernel(gpu, jl, oracle, golden, monkeypatch):
     """The log verify defaults to gv4; the stream kernel (JL_GENERAL=stream) stays covered."""
     monkeypatch.setenv("JL_GENERAL", "stream")
     test_gv4_log(gpu, jl, oracle, golden)
+
+
+@pytest.mark.parametrize("shift", [1, 16, 100, 127])
+@pytest.mark.parametrize("block_bytes", [256, 4096])
+def test_gv4_fixed_unaligned_base(gpu, jl, oracle, shift, block_bytes):
+    """Fixed stride on a base off the 128-B grid: every block gets front and tail
+    pads (the sorted pipeline with implicit offsets, not the implicit rounds)."""
+    rng = np.random.default_rng(shift * 7 + block_bytes)
+    n = 777
+    host = rng.integers(0, 256, n * block_bytes + shift, dtype=np.uint8)
+    t = to_dev(host, gpu)[shift:]
+    got = u32(jl.crc32c_fixed_dev(t, block_bytes, n))
+    assert np.array_equal(got, oracle.fixed(host[shift:], block_bytes, n, threads=THREADS))

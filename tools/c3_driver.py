@@ -16,16 +16,27 @@ torch.cuda.set_device(0)
 jl.init(0)
 dev = torch.device("cuda:0")
 rng = np.random.default_rng(SEED)
-n = 1 << 20
+n = int(os.environ.get("C3_N", 1 << 20))
 ks = np.empty(0, dtype=np.int64)
 while ks.size < n:
     k = rng.zipf(1.1, 2 * n)
     ks = np.concatenate([ks, k[k <= 64]])
 lens = (1024 * (ks[:n] - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
-if os.environ.get("C3_ALIGN"):  # study: every block 16-B aligned (lengths kept)
+if os.environ.get("C3_ROUND"):  # study: lengths rounded up to C3_ROUND bytes (aligned grid)
+    r_ = int(os.environ["C3_ROUND"])
+    lens = (((lens.astype(np.uint64) + r_ - 1) // r_) * r_).astype(np.uint32)
+if os.environ.get("C3_ALIGN"):  # study: every block C3_ALIGN-byte aligned (lengths kept)
+    al = int(os.environ["C3_ALIGN"])
     offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(((lens[:-1].astype(np.uint64) + 15) // 16) * 16, dtype=np.uint64)
+    offs[1:] = np.cumsum(((lens[:-1].astype(np.uint64) + al - 1) // al) * al, dtype=np.uint64)
     total = int(offs[-1] + lens[-1])
+elif os.environ.get("C3_SORTED"):  # study: blocks laid out in the arena in order of their step count
+    order = np.argsort((lens.astype(np.int64) + 127) // 128, kind="stable")
+    pos = np.zeros(n, np.uint64)
+    pos[1:] = np.cumsum(lens[order][:-1], dtype=np.uint64)
+    offs = np.zeros(n, np.uint64)
+    offs[order] = pos
+    total = int(lens.sum(dtype=np.uint64))
 else:
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
@@ -44,3 +55,16 @@ for i in range(L):
 torch.cuda.synchronize()
 t = [ev[i].elapsed_time(ev[i + 1]) for i in range(L)]
 print(os.environ.get("JL_GENERAL", "default"), "C3 bytes", int(lens.sum(dtype=np.uint64)), "ms", [round(x, 3) for x in t])
+if os.environ.get("C3_STREAM"):  # read ceiling over the same arena
+    sink = torch.zeros(1, dtype=torch.int32, device=dev)
+    view = arena[: (total // 4096) * 4096]
+    for _ in range(2):
+        jl.read_stream_dev(view, sink)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        jl.read_stream_dev(view, sink)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 5
+    print("read_stream bytes", view.numel(), "ms", round(ms, 3), "GB/s", round(view.numel() / ms / 1e6, 1))
