@@ -270,10 +270,13 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
     // depth (16/32/48), JL_NO_PARTITION the count split instead of bytes
     const char *e_g = getenv("JL_GENERAL");
     const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 16;
-    // general v4 (general_v4.hip): the default for the log verify (C5: 1.46x the
-    // stream kernel, r1 bench), opt-in for the other modes (JL_GENERAL=gv4; the
-    // stream kernel is faster on C3); JL_GENERAL=stream forces the stream kernel
-    const bool want_gv4 = e_g ? !strcmp(e_g, "gv4") : P.mode == jlk::MODE_LOG_VERIFY;
+    // general v4 (general_v4.hip) is the default for the crc / table-verify /
+    // log-verify modes (r1 A/B: C3 2.38 vs 2.64 ms, C5 0.81 vs 0.93 ms, C2 through
+    // offsets 0.95 vs 1.04 ms), except for small sorted batches, where its ~12
+    // pipeline launches cost more than the stream kernel's one;
+    // JL_GENERAL=stream / gv4 force either
+    const bool small = P.off && P.n < 4096;
+    const bool want_gv4 = e_g ? !strcmp(e_g, "gv4") : !small;
     if (want_gv4 && gv4_eligible(P)) return run_gv4(P, st);
     if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {
         JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));

@@ -1,5 +1,5 @@
-"""The general v4 kernel (general_v4.hip; the default for the log verify,
-JL_GENERAL=gv4 selects it for every mode) against the oracle: the variable-size, fixed-stride, table and log parity
+"""The general v4 kernel (general_v4.hip; the default general path except for
+small offset/length batches, JL_GENERAL=gv4 forces it) against the oracle: the variable-size, fixed-stride, table and log parity
 cases of test_gpu_parity.py re-run with it selected, plus cases aimed at its
 sorted-round pipeline (every K bucket, partial rounds, empty blocks mixed in,
 blocks around the 128-B step grid, a block above the solo threshold)."""
@@ -119,3 +119,17 @@ def test_gv4_fixed_unaligned_base(gpu, jl, oracle, shift, block_bytes):
     t = to_dev(host, gpu)[shift:]
     got = u32(jl.crc32c_fixed_dev(t, block_bytes, n))
     assert np.array_equal(got, oracle.fixed(host[shift:], block_bytes, n, threads=THREADS))
+
+
+@pytest.mark.parametrize("case", ["every_length", "zipf", "table"])
+def test_stream_kernel_still_exact(gpu, jl, oracle, golden, monkeypatch, case):
+    """The stream kernel (the default for small offset/length batches) on the
+    cases above, forced."""
+    monkeypatch.setenv("JL_GENERAL", "stream")
+    if case == "every_length":
+        base.test_batch_every_length_and_alignment(gpu, jl, oracle)
+    elif case == "zipf":
+        base.test_batch_large_and_zipf(gpu, jl, oracle)
+    else:
+        base.test_table_trailers_and_verify(gpu, jl, oracle, golden)
+        base.test_table_many_blocks(gpu, jl, oracle)
