@@ -422,12 +422,14 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
         const int nt = e_nt ? atoi(e_nt) : 1;
         const int depth = e_d ? atoi(e_d) : 2;
         const int chains = e_c ? atoi(e_c) : 7;  // 7 = v4 (fixed_v4.hip), measured best
-        // v4 path: 7 = 8 lanes/block, 8 = 16, 10 = 8 without nt; 11..13 = ring/occupancy study shapes 1..3
+        // v4 path: 7 = 8 lanes/block, 8-slot ring, 1024 threads (default: r1 sustained A/B 0.638 vs
+        // 0.643 ms for the 16-slot ring); 8 = 16 lanes/block; 10 = 16-slot ring without nt;
+        // 11, 12 = (8 slots, 512 threads), (16 slots, 512 threads); 13 = the 16-slot ring
         if ((chains == 7 || chains == 8 || (chains >= 10 && chains <= 13)) && ((uintptr_t)d_data & 15) == 0) {
             const int lpb = chains == 8 ? 16 : 8;
+            const int shape = chains == 7 ? 3 : (chains == 11 || chains == 12) ? chains - 10 : 0;
             JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[lpb == 4 ? 0 : lpb == 8 ? 1 : 2], (const uint8_t *)d_data,
-                                          n_blocks, flags, d_out, grid_for(n_blocks), lpb, chains != 10,
-                                          chains >= 11 ? chains - 10 : 0, st));
+                                          n_blocks, flags, d_out, grid_for(n_blocks), lpb, chains != 10, shape, st));
             return JL_OK;
         }
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,

@@ -36,7 +36,8 @@ def test_fixed_4k_random(gpu, jl, oracle, n_blocks):
     assert np.array_equal(raw, oracle.fixed(host, 4096, n_blocks, flags=0, threads=THREADS))
 
 
-FIXED_VARIANTS = {"x2": "3", "x2plain": "2", "v4_8": "7", "v4_16": "8", "v4_8_plain": "10"}
+FIXED_VARIANTS = {"x2": "3", "x2plain": "2", "v4_8": "7", "v4_16": "8", "v4_8_plain": "10", "v4_8_p8_512": "11",
+                  "v4_8_p16_512": "12", "v4_8_p16": "13"}
 
 
 @pytest.mark.parametrize("variant", sorted(FIXED_VARIANTS))
