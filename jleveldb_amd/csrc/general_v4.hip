@@ -488,10 +488,21 @@ hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_
 
 #if JL_MODE == 0
 // ---------------------------------------------------------------------------
-// Sorted pipeline: blocks -> (K, index) -> radix sort by K (host: hipcub) ->
-// run starts (max-scan of head positions) -> round heads every 8 blocks of a
-// run (sum-scan) -> GDesc table.  Blocks of K == 0 get their result here and
-// form K == 0 rounds that the main kernel skips.
+// Round pipeline (a counting sort by K; r1 replaced a 17-bit radix sort plus
+// two scans, ~20 launches, with these three):
+//   hist   per-workgroup LDS histogram of the bins b = min(K, kGSoloKey) of
+//          its chunk of blocks, flushed with one global atomic per non-empty
+//          bin (bins >= kLdsBins count globally); empty blocks get their
+//          result here and take no bin
+//   scan   one workgroup: rstart[b] = rounds of the bins before b, where a bin
+//          of c blocks has ceil(c/8) rounds (kGSoloKey: c rounds, one block
+//          each, since its blocks differ in K); total -> *n_rounds
+//   place  each workgroup recounts its chunk in LDS (the LDS atomic returns
+//          the block's rank in the chunk), reserves its ranks in every bin
+//          with one global atomic, and writes each block's GDesc at round
+//          rstart[b] + rank/8, group rank%8.
+// The order of blocks inside a bin follows the atomics, so the composition of
+// rounds varies from run to run; each block's result does not.
 // ---------------------------------------------------------------------------
 // block i: its first byte and length (fixed-stride batches that are not 128-B
 // aligned come through here too, with P.off == null)
@@ -510,72 +521,170 @@ __device__ __forceinline__ uint32_t gv4_K(uint64_t p, uint32_t n) {
     return n ? (uint32_t)(((p & 127u) + (uint64_t)n + 127u) >> 7) : 0u;
 }
 
-__global__ void gv4_keys_kernel(KParams P, uint32_t *keys, uint32_t *vals) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
+constexpr uint32_t kLdsBins = 4096;  // bins counted in LDS (K < 4096: blocks < 512 KiB)
+
+// Wave-aggregated counting: for every distinct bin among the wave's lanes, one
+// atomic adds the number of lanes in it (to the LDS counter for small bins, the
+// global one otherwise); each lane gets its rank = the atomic's old value + the
+// number of lower lanes in the same bin, so the wave's consecutive blocks of a
+// bin take consecutive ranks (rounds of neighbouring blocks).
+__device__ __forceinline__ uint32_t wave_rank(uint32_t b, uint32_t *lds_ctr, uint32_t *glob_ctr) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    uint64_t active = __builtin_amdgcn_ballot_w64(b != 0xffffffffu);
+    uint32_t rank = 0;
+    while (active) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(active);
+        const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)leader);
+        const uint64_t mask = __builtin_amdgcn_ballot_w64(b == b0);
+        uint32_t base = 0;
+        if (lane == leader) {
+            const uint32_t cnt = (uint32_t)__builtin_popcountll(mask);
+            base = b0 < kLdsBins ? atomicAdd(&lds_ctr[b0], cnt) : atomicAdd(&glob_ctr[b0], cnt);
+        }
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);
+        if (b == b0)
+            rank = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        active &= ~mask;
+    }
+    return rank;
+}
+
+__device__ __forceinline__ void gv4_chunk(uint64_t n, uint64_t &i0, uint64_t &i1) {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    i0 = (uint64_t)blockIdx.x * per;
+    i1 = i0 + per < n ? i0 + per : n;
+}
+
+// bin of block i (0xffffffff: empty block, whose result is written here:
+// extend(init, empty) = init, then the suffix byte)
+__device__ __forceinline__ uint32_t gv4_bin(const KParams &P, uint64_t i, bool write_empty) {
     uint64_t p;
     uint32_t n;
     gv4_block(P, i, p, n);
     const uint32_t K = gv4_K(p, n);
-    keys[i] = K < kGSoloKey ? K : kGSoloKey;
-    vals[i] = (uint32_t)i;
-    if (n == 0u) {  // extend(init, empty) = init (then the suffix byte)
+    if (K) return K < kGSoloKey ? K : kGSoloKey;
+    if (write_empty) {
         uint32_t st = ~(P.init ? P.init[i] : 0u);
         if (P.suffix) st = (st >> 8) ^ P.aux[(st ^ P.suffix[i]) & 0xffu];
         const uint32_t crc = ~st;
         if (P.mode == MODE_CRC) P.out32[i] = (P.flags & 1u) ? mask_crc(crc) : crc;
         else P.out8[i] = 1u;
     }
+    return 0xffffffffu;
 }
 
-__global__ void gv4_heads_kernel(const uint32_t *sk, uint64_t n, uint32_t *h) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    h[j] = (j == 0 || sk[j] != sk[j - 1] || sk[j] == kGSoloKey) ? (uint32_t)j : 0u;
+__global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, uint32_t *hist) {
+    __shared__ uint32_t h[kLdsBins];
+    for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    uint64_t i0, i1;
+    gv4_chunk(P.n, i0, i1);
+    for (uint64_t k0 = i0; k0 < i1; k0 += blockDim.x) {  // every lane runs every iteration (wave_rank)
+        const uint64_t i = k0 + threadIdx.x;
+        const uint32_t b = i < i1 ? gv4_bin(P, i, true) : 0xffffffffu;
+        wave_rank(b, h, hist);
+        if (b >= kLdsBins && b < kGSoloKey) atomicMax(&hist[kGSoloKey + 1u], b);  // rare: blocks >= 512 KiB
+    }
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x)
+        if (h[b]) {
+            atomicAdd(&hist[b], h[b]);
+            mx = b;
+        }
+    if (mx) atomicMax(&hist[kGSoloKey + 1u], mx);
 }
 
-__global__ void gv4_rhead_kernel(const uint32_t *rs, uint64_t n, uint32_t *rh) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    rh[j] = ((j - rs[j]) & 7u) == 0 ? 1u : 0u;
+// hist[kGSoloKey + 1] holds the largest non-solo bin (atomicMax in the hist kernel):
+// the scan only walks [0, that], in coalesced tiles of 4096 bins through LDS
+__global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, uint32_t *rstart, uint32_t *n_rounds) {
+    __shared__ uint32_t tile[4096];
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t nbins = hist[kGSoloKey + 1u] + 1u;  // non-solo bins [0, max]
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < nbins; t0 += 4096u) {
+        for (uint32_t k = t; k < 4096u; k += 1024u) {
+            const uint32_t c = t0 + k < nbins ? hist[t0 + k] : 0u;
+            tile[k] = (c + 7u) / 8u;  // rounds of the bin
+        }
+        __syncthreads();
+        const uint32_t r0 = tile[4 * t], r1 = tile[4 * t + 1], r2 = tile[4 * t + 2], r3 = tile[4 * t + 3];
+        const uint32_t sum = r0 + r1 + r2 + r3;
+        part[t] = sum;
+        __syncthreads();
+        for (uint32_t off = 1; off < 1024u; off <<= 1) {  // inclusive Hillis-Steele scan
+            const uint32_t v = t >= off ? part[t - off] : 0u;
+            __syncthreads();
+            part[t] += v;
+            __syncthreads();
+        }
+        const uint32_t ex = carry + part[t] - sum;
+        const uint32_t b = t0 + 4 * t;
+        if (b < nbins) rstart[b] = ex;
+        if (b + 1 < nbins) rstart[b + 1] = ex + r0;
+        if (b + 2 < nbins) rstart[b + 2] = ex + r0 + r1;
+        if (b + 3 < nbins) rstart[b + 3] = ex + r0 + r1 + r2;
+        carry += part[1023];
+        __syncthreads();  // part / tile reused by the next tile
+    }
+    if (t == 0) {  // solo blocks (>= kGSoloKey steps, any K): one round each, after all others
+        rstart[kGSoloKey] = carry;
+        *n_rounds = carry + hist[kGSoloKey];
+    }
 }
 
-__global__ void gv4_desc_kernel(KParams P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
-                                const uint32_t *rid, GDesc *desc, uint32_t *n_rounds) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= P.n) return;
-    const uint32_t i = sv[j];
-    uint64_t p;
-    uint32_t n;
-    gv4_block(P, i, p, n);
-    const uint32_t K = gv4_K(p, n);
-    const uint64_t d = K ? (uint64_t)K * 128u - (p & 127u) - n : 0u;  // tail pad, < 128
-    GDesc g;
-    g.pd = p | (d << 56);
-    g.idx = i;
-    g.K = K;
-    desc[(uint64_t)(rid[j] - 1u) * 8u + ((j - rs[j]) & 7u)] = g;
-    if (j == P.n - 1) *n_rounds = rid[j];
-    (void)sk;
+__global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, const uint32_t *rstart, uint32_t *cursor,
+                                                         GDesc *desc) {
+    __shared__ uint32_t h[kLdsBins];
+    __shared__ uint32_t base[kLdsBins];
+    for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    uint64_t i0, i1;
+    gv4_chunk(P.n, i0, i1);
+    // pass 1: ranks inside the chunk (LDS bins) or final ranks (global bins)
+    constexpr int kMaxPer = 4;  // items per thread held in registers (chunk <= 4 * 1024)
+    uint32_t rank[kMaxPer], bin[kMaxPer];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const uint64_t i = i0 + (uint64_t)k * blockDim.x + threadIdx.x;
+        bin[k] = i < i1 ? gv4_bin(P, i, false) : 0xffffffffu;
+        rank[k] = wave_rank(bin[k], h, cursor);
+    }
+    __syncthreads();
+    // reserve the chunk's ranks in every LDS bin with one global atomic
+    for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x)
+        base[b] = h[b] ? atomicAdd(&cursor[b], h[b]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMaxPer; k++) {
+        const uint32_t b = bin[k];
+        if (b == 0xffffffffu) continue;
+        const uint64_t i = i0 + (uint64_t)k * blockDim.x + threadIdx.x;
+        const uint32_t r = b < kLdsBins ? base[b] + rank[k] : rank[k];
+        uint64_t p;
+        uint32_t n;
+        gv4_block(P, i, p, n);
+        const uint32_t K = gv4_K(p, n);
+        const uint64_t d = (uint64_t)K * 128u - (p & 127u) - n;  // tail pad, < 128
+        const uint64_t round = (uint64_t)rstart[b] + (b == kGSoloKey ? r : r / 8u);
+        const uint32_t grp = b == kGSoloKey ? 0u : r % 8u;
+        GDesc g;
+        g.pd = p | (d << 56);
+        g.idx = (uint32_t)i;
+        g.K = K;
+        desc[round * 8u + grp] = g;
+    }
 }
 
-static inline dim3 grid1d(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
-
-hipError_t launch_gv4_keys(const KParams &P, uint32_t *keys, uint32_t *vals, hipStream_t st) {
-    hipLaunchKernelGGL(gv4_keys_kernel, grid1d(P.n), dim3(256), 0, st, P, keys, vals);
-    return hipGetLastError();
-}
-hipError_t launch_gv4_heads(const uint32_t *sk, uint64_t n, uint32_t *h, hipStream_t st) {
-    hipLaunchKernelGGL(gv4_heads_kernel, grid1d(n), dim3(256), 0, st, sk, n, h);
-    return hipGetLastError();
-}
-hipError_t launch_gv4_rhead(const uint32_t *rs, uint64_t n, uint32_t *rh, hipStream_t st) {
-    hipLaunchKernelGGL(gv4_rhead_kernel, grid1d(n), dim3(256), 0, st, rs, n, rh);
-    return hipGetLastError();
-}
-hipError_t launch_gv4_desc(const KParams &P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
-                           const uint32_t *rid, GDesc *desc, uint32_t *n_rounds, hipStream_t st) {
-    hipLaunchKernelGGL(gv4_desc_kernel, grid1d(P.n), dim3(256), 0, st, P, sk, sv, rs, rid, desc, n_rounds);
+hipError_t launch_gv4_rounds(const KParams &P, uint32_t *hist, uint32_t *cursor, uint32_t *rstart, GDesc *desc,
+                             uint32_t *n_rounds, hipStream_t st) {
+    // chunks of <= 4 * 1024 blocks (gv4_place_kernel keeps 4 per thread in registers)
+    const uint64_t grid = (P.n + 4095) / 4096;
+    if (grid > 0x7fffffffu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gv4_hist_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, hist);
+    hipLaunchKernelGGL(gv4_scan_kernel, dim3(1), dim3(1024), 0, st, hist, rstart, n_rounds);
+    hipLaunchKernelGGL(gv4_place_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, rstart, cursor, desc);
     return hipGetLastError();
 }
 #endif

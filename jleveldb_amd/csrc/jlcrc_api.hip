@@ -205,36 +205,22 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
         return JL_OK;
     }
     const uint64_t n = P.n;
-    // rounds: one per 8 blocks of a run, runs <= distinct K (< 2^17) + solo blocks (>= 16 MiB each)
-    const uint64_t max_rounds = (n + 7) / 8 + (1ull << 17) + 18432 + 1;
+    // rounds: ceil(c/8) per bin of c blocks <= n/8 + one partial round per bin (2^17 bins),
+    // plus one round per solo block (>= 16 MiB each: at most 18432 in 288 GiB)
+    const uint64_t nb = (uint64_t)jlk::kGSoloKey + 1;
+    const uint64_t max_rounds = n / 8 + std::min<uint64_t>(n, nb) + std::min<uint64_t>(n, 18432) + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    size_t t_sort = 0, t_max = 0, t_sum = 0;
-    uint32_t *nul = nullptr;
-    JL_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, nul, nul, nul, nul, (int)n, 0, 17, st));
-    JL_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, t_max, nul, nul, hipcub::Max(), (int)n, st));
-    JL_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, t_sum, nul, nul, (int)n, st));
-    const size_t tmp = std::max(t_sort, std::max(t_max, t_sum));
-    const size_t a4 = al(n * 4), ad = al(max_rounds * sizeof(jlk::GDesc) * 8);
-    const size_t total = 6 * a4 + ad + 256 + al(tmp);
+    const size_t ab = al((nb + 1) * 4), ad = al(max_rounds * sizeof(jlk::GDesc) * 8);  // hist[nb] = max bin
+    const size_t total = 3 * ab + ad + 256;
     char *buf = nullptr;
     if (hipMallocAsync((void **)&buf, total, st) != hipSuccess) return fail(JL_ERR_NOMEM, "gv4 scratch allocation failed");
-    uint32_t *keys = (uint32_t *)buf, *vals = (uint32_t *)(buf + a4), *sk = (uint32_t *)(buf + 2 * a4),
-             *sv = (uint32_t *)(buf + 3 * a4), *rs = (uint32_t *)(buf + 4 * a4), *rid = (uint32_t *)(buf + 5 * a4);
-    jlk::GDesc *desc = (jlk::GDesc *)(buf + 6 * a4);
-    uint32_t *n_rounds = (uint32_t *)(buf + 6 * a4 + ad);
-    void *t = buf + 6 * a4 + ad + 256;
-    hipError_t e = hipSuccess;
-    size_t ts = tmp;
+    uint32_t *hist = (uint32_t *)buf, *cursor = (uint32_t *)(buf + ab), *rstart = (uint32_t *)(buf + 2 * ab);
+    jlk::GDesc *desc = (jlk::GDesc *)(buf + 3 * ab);
+    uint32_t *n_rounds = (uint32_t *)(buf + 3 * ab + ad);
+    hipError_t e = hipMemsetAsync(buf, 0, 2 * ab, st);  // hist, cursor
+    // null groups of partial rounds: idx = kGNull (the kernel mirrors group 0 there)
     if (e == hipSuccess) e = hipMemsetAsync(desc, 0xff, max_rounds * sizeof(jlk::GDesc) * 8, st);
-    if (e == hipSuccess) e = jlk::launch_gv4_keys(P, keys, vals, st);
-    if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortPairs(t, ts, keys, sk, vals, sv, (int)n, 0, 17, st);
-    if (e == hipSuccess) e = jlk::launch_gv4_heads(sk, n, keys, st);  // keys <- head positions
-    ts = tmp;
-    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveScan(t, ts, keys, rs, hipcub::Max(), (int)n, st);
-    if (e == hipSuccess) e = jlk::launch_gv4_rhead(rs, n, vals, st);  // vals <- round-head flags
-    ts = tmp;
-    if (e == hipSuccess) e = hipcub::DeviceScan::InclusiveSum(t, ts, vals, rid, (int)n, st);
-    if (e == hipSuccess) e = jlk::launch_gv4_desc(P, sk, sv, rs, rid, desc, n_rounds, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_rounds(P, hist, cursor, rstart, desc, n_rounds, st);
     A.desc = desc;
     A.n_rounds = n_rounds;
     unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];

@@ -82,11 +82,8 @@ hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream
 template <int MODE>
 hipError_t launch_gv4_m(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st);
 // sorted-pipeline helpers (general_v4.hip, mode-0 object)
-hipError_t launch_gv4_keys(const KParams &P, uint32_t *keys, uint32_t *vals, hipStream_t st);
-hipError_t launch_gv4_heads(const uint32_t *sk, uint64_t n, uint32_t *h, hipStream_t st);
-hipError_t launch_gv4_rhead(const uint32_t *rs, uint64_t n, uint32_t *rh, hipStream_t st);
-hipError_t launch_gv4_desc(const KParams &P, const uint32_t *sk, const uint32_t *sv, const uint32_t *rs,
-                           const uint32_t *rid, GDesc *desc, uint32_t *n_rounds, hipStream_t st);
+hipError_t launch_gv4_rounds(const KParams &P, uint32_t *hist, uint32_t *cursor, uint32_t *rstart, GDesc *desc,
+                             uint32_t *n_rounds, hipStream_t st);
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
 template <int MODE>
