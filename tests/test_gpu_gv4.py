@@ -133,3 +133,22 @@ def test_stream_kernel_still_exact(gpu, jl, oracle, golden, monkeypatch, case):
     else:
         base.test_table_trailers_and_verify(gpu, jl, oracle, golden)
         base.test_table_many_blocks(gpu, jl, oracle)
+
+
+def test_gv4_rounds_pipeline_large_bins(gpu, jl, oracle):
+    """Blocks of 512 KiB .. 1.5 MiB (steps >= 4096: the global-atomic bins, and
+    the scan's second and later 4096-bin tiles) mixed with small ones and
+    repeated lengths (partial rounds of one bin), in one batch."""
+    rng = np.random.default_rng(24)
+    big = [int(x) for x in rng.integers(512 << 10, 1536 << 10, 12)]
+    lens = np.array(big + [big[0]] * 9 + [7, 0, 1000, 4096, 129] * 5, np.uint32)
+    rng.shuffle(lens)
+    offs = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i in range(lens.size):
+        pos += int(rng.integers(0, 64))
+        offs[i] = pos
+        pos += int(lens[i])
+    arena = rng.integers(0, 256, pos + 8, dtype=np.uint8)
+    got = u32(jl.crc32c_batch_dev(to_dev(arena, gpu), to_dev(offs.view(np.int64), gpu), to_dev(lens.view(np.int32), gpu)))
+    assert np.array_equal(got, oracle.batch(arena, offs, lens, threads=THREADS))
