@@ -163,7 +163,8 @@ constexpr size_t kV4UDword = 36864;
 constexpr size_t kV4SlotDword = 37248;
 constexpr size_t kG4UDword = 38272;
 constexpr size_t kG4T0Dword = 39296;
-constexpr size_t kG4DDword = 39552;  // 7 x 128 dwords, ends at 40448 <= kImageDwords
+constexpr size_t kG4ShiftDword = 36864;  // gv4 image: 7 x 128 dwords (replaces the v4 U4 tables)
+constexpr size_t kG4EDword = 37760;      // gv4 image: 4 x 128 dwords, ends at 38272 = kG4UDword
 inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     const Tables &T = tables();
     const int gap = 16 * lpb - 4;
@@ -184,10 +185,30 @@ inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     for (int j = 0; j < 4; j++)
         for (uint32_t v = 0; v < 256; v++) img[kG4UDword + 256 * j + v] = slice4_inv(v << (8 * j));
     for (int i = 0; i < 256; i++) img[kG4T0Dword + i] = T.t[0][i];
-    for (int u = 0; u < 7; u++)  // z^-(2^u): removes a tail pad of d bytes bit by bit
+    return img;
+}
+
+// General v4 image (general_v4.hip): the v4 image for 8 lanes per block with
+// the epilogue tables re-cut so a block's tail pad d = 16a + 4c + e folds into
+// shifts the epilogue does anyway:
+//   lane tables   column b: z^-(16 (b % 16))   (realign by 16 (l + a))
+//   kG4ShiftDword U_k = z^-(4k), k = 0..6       (chain j: z^-(4 (j + c)))
+//   kG4EDword     E_e = z^-e, e = 0..3          (after the group xor)
+inline std::vector<uint32_t> build_lds_image_gv4() {
+    const Tables &T = tables();
+    std::vector<uint32_t> img = build_lds_image_v4(8);
+    for (int b = 0; b < 32; b++)
         for (int p = 0; p < 8; p++)
             for (int v = 0; v < 16; v++)
-                img[kG4DDword + (size_t)u * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 1ull << u);
+                img[32768 + (size_t)(p * 16 + v) * 32 + b] = T.zinvn((uint32_t)v << (4 * p), 16u * (uint32_t)(b % 16));
+    for (int k = 0; k < 7; k++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kG4ShiftDword + (size_t)k * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 4u * (uint32_t)k);
+    for (int e = 0; e < 4; e++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kG4EDword + (size_t)e * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), (uint32_t)e);
     return img;
 }
 

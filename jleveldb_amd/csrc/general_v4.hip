@@ -231,7 +231,6 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
     const GLanes gl(lane);
-    const uint32_t lc = 131072u | ((lane & 31u) << 2);
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t w = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
     const uint64_t R = A.desc ? (uint64_t)*A.n_rounds : (A.P.n + 7u) / 8u;
@@ -333,20 +332,18 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     };
     // end of a round: epilogue, result, next round of the compute cursor; false when done
     auto finish = [&]() -> bool {
+        // chain (l, j) ends at 16 l + 4 j past the last window, the window ends d
+        // = 16 a + 4 c + e bytes past the block: shift by z^-(4 (j + c)), then by
+        // z^-(16 (l + a)) (lane tables), group xor, then z^-e
+        const uint32_t d = cv.d, sa = 512u * ((d >> 2) & 3u);
         const uint32_t s0 = gstep_x3(lds, x0, gl, 0u), s1 = gstep_x3(lds, x1, gl, 0u);
         const uint32_t s2 = gstep_x3(lds, x2, gl, 0u), s3 = gstep_x3(lds, x3, gl, 0u);
-        const uint32_t c = xor3(s0, ushift(lds, s1, kV4U4Byte), ushift(lds, s2, kV4U4Byte + 512u)) ^
-                           ushift(lds, s3, kV4U4Byte + 1024u);
-        uint32_t st = group_xor<8>(realign(lds, c, lc));
-        // undo the tail pad: st is the state after d zero bytes past the block
-#pragma unroll
-        for (int i = 0; i < 7; i++) {
-            const bool bit = (cv.d >> i) & 1u;
-            if (__builtin_amdgcn_ballot_w64(bit)) {
-                const uint32_t sh = ushift(lds, st, kG4DByte + 512u * i);
-                st = bit ? sh : st;
-            }
-        }
+        const uint32_t c = xor3(ushift(lds, s0, kG4ShiftByte + sa), ushift(lds, s1, kG4ShiftByte + 512u + sa),
+                                ushift(lds, s2, kG4ShiftByte + 1024u + sa)) ^
+                           ushift(lds, s3, kG4ShiftByte + 1536u + sa);
+        const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
+        uint32_t st = group_xor<8>(realign(lds, c, 131072u | (col << 2)));
+        st = ushift(lds, st, kG4EByte + 512u * (d & 3u));
         // side chunks of lanes 0 and 1 of the group, seen from lane 0 (DPP row_shl:1)
         const uint32_t h0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.x, 0x101, 0xf, 0xf, false);
         const uint32_t h1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.y, 0x101, 0xf, 0xf, false);

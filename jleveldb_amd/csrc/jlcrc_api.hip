@@ -62,7 +62,7 @@ struct Context {
     int cus = 0;
     hipStream_t stream = nullptr;
     void *d_img = nullptr;   // 160 KiB LDS image
-    void *d_img_v4[3] = {nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block
+    void *d_img_v4[4] = {nullptr, nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block; [3] gv4
     uint32_t *d_aux = nullptr;
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
@@ -184,7 +184,7 @@ static bool gv4_eligible(const jlk::KParams &P) {
 }
 
 static hipError_t gv4_launch(const jlk::GV4Args &A, hipStream_t st) {
-    const void *img = ctx().d_img_v4[1];  // 8 lanes per block
+    const void *img = ctx().d_img_v4[3];  // the general v4 image (crc_math.hpp)
     const int grid = ctx().cus;            // one 512-thread workgroup per CU (the LDS image)
     switch (A.P.mode) {
     case jlk::MODE_CRC: return jlk::launch_gv4_m<jlk::MODE_CRC>(img, A, ctx().d_zero, grid, st);
@@ -346,8 +346,8 @@ int jl_init(int device) {
     JL_HIP(hipMalloc((void **)&c.d_zero, 4096));
     JL_HIP(hipMalloc((void **)&c.d_scratch, 4096));
     JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
-    for (int i = 0; i < 3; i++) {
-        std::vector<uint32_t> v4 = jlmath::build_lds_image_v4(4 << i);
+    for (int i = 0; i < 4; i++) {
+        std::vector<uint32_t> v4 = i < 3 ? jlmath::build_lds_image_v4(4 << i) : jlmath::build_lds_image_gv4();
         JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
         JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     }

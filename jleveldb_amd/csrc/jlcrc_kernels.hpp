@@ -12,7 +12,8 @@ constexpr uint32_t kV4U4Byte = 147456;   // uniform z^-4, z^-8, z^-12 nibble tab
 constexpr uint32_t kV4SlotDword = 37248; // per-wave result slots (64 dwords per wave)
 constexpr uint32_t kG4UByte = 153088;    // general v4: U_j[v] = slice4^-1(v << 8j), 4 x 256 dwords (seed of an init)
 constexpr uint32_t kG4T0Byte = 157184;   // general v4: T0 (suffix byte step)
-constexpr uint32_t kG4DByte = 158208;    // general v4: z^-(2^i), i = 0..6, nibble tables (tail-pad removal)
+constexpr uint32_t kG4ShiftByte = 147456;  // general v4 image: U_k = z^-(4k), k = 0..6, nibble tables
+constexpr uint32_t kG4EByte = 151040;      // general v4 image: E_e = z^-e, e = 0..3, nibble tables
 constexpr uint32_t kGNull = 0xffffffffu; // general v4: empty group of a round
 
 enum : int {

@@ -111,6 +111,50 @@ static uint32_t emulate_v4(const std::vector<uint32_t>& img, const uint8_t* blk,
     return ~total;
 }
 
+// The general v4 kernel (general_v4.hip) on its 128-B aligned grid: block at
+// offset f of its first window, K = ceil((f+n)/128) windows, tail pad d; the
+// seed word W at virtual bytes [f-4, f) (chain lane 7 / dword 3 starts from
+// gstep(W << 8f) when f < 4); epilogue with the gv4 image's U_{j+c}, lane
+// column (l + a) & 15 | (q & 1) << 4 and E_e, d = 16a + 4c + e.
+static uint32_t nib(const std::vector<uint32_t>& img, size_t base_dw, uint32_t s) {
+    uint32_t r = 0;
+    for (int p = 0; p < 8; p++) r ^= img[base_dw + p * 16 + ((s >> (4 * p)) & 15)];
+    return r;
+}
+
+static uint32_t emulate_gv4(const std::vector<uint32_t>& img, const uint8_t* blk, uint32_t n, uint32_t f, uint32_t init,
+                            int q) {
+    if (n == 0) return init;
+    const uint32_t K = (f + n + 127) / 128, d = 128 * K - f - n, W = slice4_inv(~init);
+    std::vector<uint8_t> V(128 * K + 4, 0);  // V[t + 4] = virtual byte t, t >= -4
+    for (int t = -4; t < (int)(128 * K); t++) {
+        uint8_t b = 0;
+        if (t >= (int)f && t < (int)(f + n)) b = blk[t - f];
+        else if (t >= (int)f - 4 && t < (int)f) b = (uint8_t)(W >> (8 * (t - (int)f + 4)));
+        V[t + 4] = b;
+    }
+    uint32_t total = 0;
+    for (int l = 0; l < 8; l++) {
+        const int lane = q * 8 + l;
+        uint32_t c = 0;
+        for (int j = 0; j < 4; j++) {
+            uint32_t s = 0;
+            for (int k = -1; k < (int)K; k++) {
+                const int pos = 128 * k + 16 * l + 4 * j;
+                uint32_t w = 0;
+                if (pos >= -4) memcpy(&w, &V[pos + 4], 4);
+                s = gstep_img(img, s ^ w, lane);
+            }
+            c ^= nib(img, kG4ShiftDword + 128 * (j + ((d >> 2) & 3)), s);
+        }
+        const uint32_t col = ((l + (d >> 4)) & 15) | ((q & 1) << 4);
+        uint32_t r = 0;
+        for (int p = 0; p < 8; p++) r ^= img[32768 + (p * 16 + ((c >> (4 * p)) & 15)) * 32 + col];
+        total ^= r;
+    }
+    return ~nib(img, kG4EDword + 128 * (d & 3), total);
+}
+
 int main() {
     auto img = build_lds_image();
     std::mt19937_64 rng(42);
@@ -143,6 +187,19 @@ int main() {
             cases++;
             if (want != got && bad++ < 10) printf("v4 mismatch lpb=%d q=%d %08x %08x\n", lpb, q, want, got);
         }
+    }
+    {
+        auto imgg = build_lds_image_gv4();
+        for (uint32_t n = 0; n <= 700; n++)
+            for (uint32_t f : {0u, 1u, 3u, 4u, 5u, 17u, 63u, 100u, 124u, 127u}) {
+                const uint32_t init = (n % 5 == 0) ? 0u : (uint32_t)rng();
+                const int q = (int)((n + f) % 8);
+                const uint8_t* blk = buf.data() + (n * 7 + f) % 5000;
+                const uint32_t want = ~ref_update(~init, blk, n);
+                const uint32_t got = emulate_gv4(imgg, blk, n, f, init, q);
+                cases++;
+                if (want != got && bad++ < 10) printf("gv4 mismatch n=%u f=%u q=%d %08x %08x\n", n, f, q, want, got);
+            }
     }
     printf("%d cases, %d mismatches\n", cases, bad);
     return bad != 0;

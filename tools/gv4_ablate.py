@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Timing-only ablation of the gv4 round machinery (JL_GV4_ABL=3: no tail-pad
+correction, 4: no compute-cursor descriptor reload, 5: no epilogue lookups;
+results of 3-5 are wrong by construction).  Workloads: 4M blocks of 1057 B at
+1064-B spacing (C5 record shape, offset/length batch) and 4M x 1 KiB implicit
+rounds."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import jleveldb_amd as jl  # noqa: E402
+
+os.environ["JL_GENERAL"] = "gv4"
+torch.cuda.set_device(0)
+jl.init(0)
+dev = torch.device("cuda:0")
+n = 4 << 20
+arena = torch.empty(n * 1064 + 64, dtype=torch.uint8, device=dev)
+jl.fill_random_dev(arena, 9)
+off = torch.arange(n, dtype=torch.int64, device=dev) * 1064 + 7
+ln = torch.full((n,), 1057, dtype=torch.int32, device=dev)
+out = torch.empty(n, dtype=torch.int32, device=dev)
+
+
+def t_of(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+res = {}
+for rnd in range(2):
+    for v in ["", "3", "4", "5"]:
+        if v:
+            os.environ["JL_GV4_ABL"] = v
+        else:
+            os.environ.pop("JL_GV4_ABL", None)
+        a = t_of(lambda: jl.crc32c_batch_dev(arena, off, ln, out=out))
+        b = t_of(lambda: jl.crc32c_fixed_dev(arena, 1024, n, out=out))
+        res.setdefault(v or "base", []).append((round(a, 4), round(b, 4)))
+for k, v in res.items():
+    print(json.dumps({"variant": k, "c5shape_ms": [x[0] for x in v], "implicit1k_ms": [x[1] for x in v]}))
