@@ -445,7 +445,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         JL_XS4(R0, R1, R2, R3)                                                                             \
         JL_GLD(RQ, pf.addr, 128 * (u), R0, R1, R2, R3)                                                     \
     }
-    const bool fast_ok = !A.P.dbg;
+    const bool fast_ok = !A.P.dbg && !A.no_fast;
     for (;;) {
         if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
             pf.e + (uint32_t)P_ < pf.E) {

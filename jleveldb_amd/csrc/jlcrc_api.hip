@@ -198,6 +198,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     memset(&A, 0, sizeof(A));
     A.P = P;
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
+    A.no_fast = getenv("JL_GV4_NOFAST") ? 1u : 0u;
     if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0) {
         // every block starts on the 128-B grid: implicit rounds, no pads, no sort
         A.fixed_K = (uint32_t)(P.fixed_bytes / 128);

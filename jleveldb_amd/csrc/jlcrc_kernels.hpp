@@ -60,6 +60,7 @@ struct GV4Args {
     const uint32_t *n_rounds;   // device count of rounds (sorted pipeline)
     uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
     uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
+    uint32_t no_fast;           // study (JL_GV4_NOFAST): every ring turn takes the per-entry path
 };
 constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
 

@@ -1,9 +1,7 @@
 #!/usr/bin/env python3
-"""Timing-only ablation of the gv4 round machinery (JL_GV4_ABL=3: no tail-pad
-correction, 4: no compute-cursor descriptor reload, 5: no epilogue lookups;
-results of 3-5 are wrong by construction).  Workloads: 4M blocks of 1057 B at
-1064-B spacing (C5 record shape, offset/length batch) and 4M x 1 KiB implicit
-rounds."""
+"""gv4 per-entry path cost: the same batches with fast ring turns allowed and
+disabled (JL_GV4_NOFAST).  Workloads: 4M blocks of 1057 B at 1064-B spacing
+(C5 record shape), 4M x 1 KiB implicit rounds, 512 x 8 MiB blocks (long rounds)."""
 import json
 import os
 import sys
@@ -38,14 +36,18 @@ def t_of(fn, reps=10):
 
 
 res = {}
+big = 8 << 20
+nbig = arena.numel() // big
 for rnd in range(2):
-    for v in ["", "3", "4", "5"]:
+    for v in ["", "nofast"]:
         if v:
-            os.environ["JL_GV4_ABL"] = v
+            os.environ["JL_GV4_NOFAST"] = "1"
         else:
-            os.environ.pop("JL_GV4_ABL", None)
+            os.environ.pop("JL_GV4_NOFAST", None)
         a = t_of(lambda: jl.crc32c_batch_dev(arena, off, ln, out=out))
         b = t_of(lambda: jl.crc32c_fixed_dev(arena, 1024, n, out=out))
-        res.setdefault(v or "base", []).append((round(a, 4), round(b, 4)))
+        c = t_of(lambda: jl.crc32c_fixed_dev(arena, big, nbig, out=out))
+        res.setdefault(v or "base", []).append((round(a, 4), round(b, 4), round(c, 4)))
 for k, v in res.items():
-    print(json.dumps({"variant": k, "c5shape_ms": [x[0] for x in v], "implicit1k_ms": [x[1] for x in v]}))
+    print(json.dumps({"variant": k, "c5shape_ms": [x[0] for x in v], "implicit1k_ms": [x[1] for x in v],
+                      "blocks8M_ms": [x[2] for x in v]}))
