@@ -219,7 +219,10 @@ inline std::vector<uint32_t> build_lds_image_gv4() {
 //   [520,525)   W(typeCrc[t]) = slice4^-1(~typeCrc[t])   (stream-kernel seeds)
 //   [525]       W(0) = slice4^-1(0xffffffff)               (value(): init 0)
 //   [528,1552)  U_j[v] = slice4^-1(v << 8j), j = 0..3     (seed of an arbitrary init)
-constexpr size_t kAuxDwords = 1552;
+//   [1552,5648) Z_k = z^(2^k), k = 0..31, nibble tables (8 x 16 each): the state
+//               shift by 2^k zero bytes (folding the chunks of a split block)
+constexpr size_t kAuxZpow = 1552;
+constexpr size_t kAuxDwords = kAuxZpow + 32 * 128;
 inline std::vector<uint32_t> build_aux() {
     const Tables &T = tables();
     std::vector<uint32_t> aux(kAuxDwords, 0);
@@ -232,6 +235,21 @@ inline std::vector<uint32_t> build_aux() {
     aux[525] = slice4_inv(0xffffffffu);
     for (int j = 0; j < 4; j++)
         for (uint32_t v = 0; v < 256; v++) aux[528 + 256 * j + v] = slice4_inv(v << (8 * j));
+    // z^(2^k) by repeated squaring of the 32x32 GF(2) matrix of z (column b = z(e_b))
+    uint32_t col[32], sq[32];
+    for (int b = 0; b < 32; b++) col[b] = T.z(1u << b);
+    auto apply = [](const uint32_t *m, uint32_t v) {
+        uint32_t r = 0;
+        for (int b = 0; b < 32; b++)
+            if ((v >> b) & 1u) r ^= m[b];
+        return r;
+    };
+    for (int k = 0; k < 32; k++) {
+        for (int p = 0; p < 8; p++)
+            for (uint32_t v = 0; v < 16; v++) aux[kAuxZpow + 128 * k + 16 * p + v] = apply(col, v << (4 * p));
+        for (int b = 0; b < 32; b++) sq[b] = apply(col, col[b]);
+        for (int b = 0; b < 32; b++) col[b] = sq[b];
+    }
     return aux;
 }
 

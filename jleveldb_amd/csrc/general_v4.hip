@@ -165,8 +165,9 @@ struct GPF {
             c0 = sa & ~(uint64_t)15;
             c1 = (sa + 3u) & ~(uint64_t)15;
         } else {
-            if (A.P.init && v.idx != kGNull) c0 = (uint64_t)(uintptr_t)(A.P.init + v.idx) & ~(uint64_t)15;
-            if (A.P.suffix && v.idx != kGNull) c1 = (uint64_t)(uintptr_t)(A.P.suffix + v.idx) & ~(uint64_t)15;
+            // real blocks only (idx < kGPart): chunk groups of a split block and empty groups load nothing
+            if (A.P.init && v.idx < kGPart) c0 = (uint64_t)(uintptr_t)(A.P.init + v.idx) & ~(uint64_t)15;
+            if (A.P.suffix && v.idx < kGPart) c1 = (uint64_t)(uintptr_t)(A.P.suffix + v.idx) & ~(uint64_t)15;
         }
         side_addr = l == 0u ? c0 : (l == 1u ? c1 : dummy);
         e = 0;
@@ -308,6 +309,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
                     lds_at(lds, kG4UByte + 2048u + (((y >> 16) & 0xffu) << 2)) ^
                     lds_at(lds, kG4UByte + 3072u + ((y >> 24) << 2));
             }
+            if (MODE == MODE_CRC && cv.idx >= kGPart) W = 0u;  // chunk of a split block: from state 0
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int t = (int)(16u * l + 4u * j) - (int)f;  // dword start relative to p
@@ -350,6 +352,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.z, 0x101, 0xf, 0xf, false);
         const uint32_t h3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.w, 0x101, 0xf, 0xf, false);
         const uint64_t p = cv.p;
+        const uint32_t raw = st;  // chunk groups of a split block report the raw state
         if (!GV4<MODE>::VERIFY && A.P.suffix) {
             const uint64_t sa = (uint64_t)(uintptr_t)(A.P.suffix + (cv.idx == kGNull ? 0u : cv.idx));
             const uint32_t k = (uint32_t)(sa >> 2) & 3u;
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
             st = (st >> 8) ^ lds_at(lds, kG4T0Byte + (((st ^ sfx) & 0xffu) << 2));
         }
         const uint32_t crc = ~st, m = mask_crc(crc);
-        if (A.P.dbg && l == 0u && cv.idx != kGNull && cv.idx >= A.P.n) {
+        if (A.P.dbg && l == 0u && cv.idx < kGPart && cv.idx >= A.P.n) {
             const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
             if (slot < 256) {
                 A.P.dbg[1 + 4 * slot] = cr;
@@ -368,7 +371,8 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
             }
         } else if (l == 0u && cv.idx != kGNull) {
             if (MODE == MODE_CRC) {
-                A.P.out32[cv.idx] = (A.P.flags & 1u) ? m : crc;
+                if (cv.idx >= kGPart) A.parts[cv.idx - kGPart] = raw;
+                else A.P.out32[cv.idx] = (A.P.flags & 1u) ? m : crc;
             } else {
                 const uint32_t n = cK * 128u - (uint32_t)(p & 127u) - cv.d;
                 const uint64_t sa = MODE == MODE_LOG_VERIFY ? p - 6u : p + n;
@@ -570,7 +574,36 @@ __device__ __forceinline__ uint32_t gv4_bin(const KParams &P, uint64_t i, bool w
     return 0xffffffffu;
 }
 
-__global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, uint32_t *hist) {
+// Split geometry of a block of n bytes (MODE_CRC, n > kGSplitMin): m <= 2048
+// chunks of cs bytes (a multiple of 128, >= 64 KiB), the last one shorter.
+// Every chunk starts at the block's offset in its 128-B window.
+__device__ __forceinline__ bool gv4_split_geom(const KParams &P, const GSplit &S, uint32_t n, uint32_t &cs,
+                                               uint32_t &m) {
+    if (!S.part_cap || P.mode != MODE_CRC || (uint64_t)n <= kGSplitMin) return false;
+    uint64_t c = ((uint64_t)n + 2047u) / 2048u;
+    c = (c + 127u) & ~(uint64_t)127;
+    if (c < (64u << 10)) c = 64u << 10;
+    cs = (uint32_t)c;
+    m = (uint32_t)(((uint64_t)n + c - 1u) / c);
+    return true;
+}
+
+// bins and tail pads of a split block's full chunks (F) and last chunk (L)
+struct GChunks {
+    uint32_t kF, kL, dF, dL, L;
+};
+__device__ __forceinline__ GChunks gv4_chunks(uint64_t p, uint32_t n, uint32_t cs, uint32_t m) {
+    GChunks g;
+    const uint32_t f = (uint32_t)(p & 127u);
+    g.L = n - (m - 1u) * cs;
+    g.kF = (f + cs + 127u) >> 7;
+    g.kL = (f + g.L + 127u) >> 7;
+    g.dF = 128u * g.kF - f - cs;
+    g.dL = 128u * g.kL - f - g.L;
+    return g;
+}
+
+__global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uint32_t *hist) {
     __shared__ uint32_t h[kLdsBins];
     for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x) h[b] = 0;
     __syncthreads();
@@ -578,7 +611,31 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, uint32_t *his
     gv4_chunk(P.n, i0, i1);
     for (uint64_t k0 = i0; k0 < i1; k0 += blockDim.x) {  // every lane runs every iteration (wave_rank)
         const uint64_t i = k0 + threadIdx.x;
-        const uint32_t b = i < i1 ? gv4_bin(P, i, true) : 0xffffffffu;
+        uint32_t b = 0xffffffffu;
+        if (i < i1) {
+            uint64_t p;
+            uint32_t n, cs, m;
+            gv4_block(P, i, p, n);
+            bool split = false;
+            if (gv4_split_geom(P, S, n, cs, m)) {  // rare: blocks > 512 KiB
+                const unsigned long long base = atomicAdd(&S.ctl[0], (unsigned long long)m);
+                split = base + m <= S.part_cap;
+                S.bigbase[i] = split ? (uint32_t)base : 0xffffffffu;
+                if (split) {
+                    const uint32_t bid = (uint32_t)atomicAdd(&S.ctl[1], 1ull);
+                    GBig g;
+                    g.i = i;
+                    g.part0 = (uint32_t)base;
+                    g.m = m;
+                    S.big[bid] = g;
+                    const GChunks c = gv4_chunks(p, n, cs, m);
+                    if (m > 1u) atomicAdd(&hist[c.kF], m - 1u);
+                    atomicAdd(&hist[c.kL], 1u);
+                    atomicMax(&hist[kGSoloKey + 1u], c.kF > c.kL ? c.kF : c.kL);
+                }
+            }
+            if (!split) b = gv4_bin(P, i, true);
+        }
         wave_rank(b, h, hist);
         if (b >= kLdsBins && b < kGSoloKey) atomicMax(&hist[kGSoloKey + 1u], b);  // rare: blocks >= 512 KiB
     }
@@ -631,7 +688,20 @@ __global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, ui
     }
 }
 
-__global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, const uint32_t *rstart, uint32_t *cursor,
+__device__ __forceinline__ void gv4_put(GDesc *desc, const uint32_t *rstart, uint32_t b, uint32_t r, uint64_t p,
+                                        uint64_t d, uint32_t idx, uint32_t K) {
+    const uint64_t round = (uint64_t)rstart[b] + (b == kGSoloKey ? r : r / 8u);
+    const uint32_t grp = b == kGSoloKey ? 0u : r % 8u;
+    GDesc g;
+    g.pd = p | (d << 56);
+    g.idx = idx;
+    g.K = K;
+    desc[round * 8u + grp] = g;
+}
+
+constexpr uint32_t kSplitBin = 0xfffffffeu;  // place kernel: a split block (its chunks go to their bins)
+
+__global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, GSplit S, const uint32_t *rstart, uint32_t *cursor,
                                                          GDesc *desc) {
     __shared__ uint32_t h[kLdsBins];
     __shared__ uint32_t base[kLdsBins];
@@ -645,8 +715,14 @@ __global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, const uint32
 #pragma unroll
     for (int k = 0; k < kMaxPer; k++) {
         const uint64_t i = i0 + (uint64_t)k * blockDim.x + threadIdx.x;
-        bin[k] = i < i1 ? gv4_bin(P, i, false) : 0xffffffffu;
-        rank[k] = wave_rank(bin[k], h, cursor);
+        bin[k] = 0xffffffffu;
+        if (i < i1) {
+            uint64_t p;
+            uint32_t n, cs, m;
+            gv4_block(P, i, p, n);
+            bin[k] = gv4_split_geom(P, S, n, cs, m) && S.bigbase[i] != 0xffffffffu ? kSplitBin : gv4_bin(P, i, false);
+        }
+        rank[k] = wave_rank(bin[k] == kSplitBin ? 0xffffffffu : bin[k], h, cursor);
     }
     __syncthreads();
     // reserve the chunk's ranks in every LDS bin with one global atomic
@@ -658,30 +734,91 @@ __global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, const uint32
         const uint32_t b = bin[k];
         if (b == 0xffffffffu) continue;
         const uint64_t i = i0 + (uint64_t)k * blockDim.x + threadIdx.x;
-        const uint32_t r = b < kLdsBins ? base[b] + rank[k] : rank[k];
         uint64_t p;
         uint32_t n;
         gv4_block(P, i, p, n);
+        if (b == kSplitBin) {  // chunks 0..m-2 of cs bytes and the last one, each its own group
+            uint32_t cs, m;
+            gv4_split_geom(P, S, n, cs, m);
+            const GChunks c = gv4_chunks(p, n, cs, m);
+            const uint32_t part0 = S.bigbase[i];
+            const uint32_t rF = m > 1u ? atomicAdd(&cursor[c.kF], m - 1u) : 0u, rL = atomicAdd(&cursor[c.kL], 1u);
+            for (uint32_t j = 0; j + 1u < m; j++)
+                gv4_put(desc, rstart, c.kF, rF + j, p + (uint64_t)j * cs, c.dF, kGPart | (part0 + j), c.kF);
+            gv4_put(desc, rstart, c.kL, rL, p + (uint64_t)(m - 1u) * cs, c.dL, kGPart | (part0 + m - 1u), c.kL);
+            continue;
+        }
+        const uint32_t r = b < kLdsBins ? base[b] + rank[k] : rank[k];
         const uint32_t K = gv4_K(p, n);
-        const uint64_t d = (uint64_t)K * 128u - (p & 127u) - n;  // tail pad, < 128
-        const uint64_t round = (uint64_t)rstart[b] + (b == kGSoloKey ? r : r / 8u);
-        const uint32_t grp = b == kGSoloKey ? 0u : r % 8u;
-        GDesc g;
-        g.pd = p | (d << 56);
-        g.idx = (uint32_t)i;
-        g.K = K;
-        desc[round * 8u + grp] = g;
+        gv4_put(desc, rstart, b, r, p, (uint64_t)K * 128u - (p & 127u) - n, (uint32_t)i, K);
     }
 }
 
-hipError_t launch_gv4_rounds(const KParams &P, uint32_t *hist, uint32_t *cursor, uint32_t *rstart, GDesc *desc,
-                             uint32_t *n_rounds, hipStream_t st) {
+hipError_t launch_gv4_rounds(const KParams &P, const GSplit &S, uint32_t *hist, uint32_t *cursor, uint32_t *rstart,
+                             GDesc *desc, uint32_t *n_rounds, hipStream_t st) {
     // chunks of <= 4 * 1024 blocks (gv4_place_kernel keeps 4 per thread in registers)
     const uint64_t grid = (P.n + 4095) / 4096;
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gv4_hist_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, hist);
+    hipLaunchKernelGGL(gv4_hist_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, S, hist);
     hipLaunchKernelGGL(gv4_scan_kernel, dim3(1), dim3(1024), 0, st, hist, rstart, n_rounds);
-    hipLaunchKernelGGL(gv4_place_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, rstart, cursor, desc);
+    hipLaunchKernelGGL(gv4_place_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, S, rstart, cursor, desc);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Split blocks: state(A || B) = z^|B|(state(A)) ^ state_0(B) over GF(2), where
+// state_0 starts from 0 and z^L, L zero bytes, is applied bit by bit of L with
+// the z^(2^k) nibble tables in aux.  One wave per split block: lane t folds its
+// consecutive chunks, a 6-level tree folds the lanes, lane 0 adds the init
+// (update(~init, D) = z^|D|(~init) ^ state_0(D)), the suffix byte and the mask.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t gv4_zpow(const uint32_t *aux, uint32_t s, uint32_t L) {
+    while (L) {
+        const uint32_t *t = aux + kAuxZpowDword + 128u * (uint32_t)__builtin_ctz(L);
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) r ^= t[16 * q + ((s >> (4 * q)) & 15u)];
+        s = r;
+        L &= L - 1u;
+    }
+    return s;
+}
+
+__global__ __launch_bounds__(64) void gv4_combine_kernel(KParams P, GSplit S, const uint32_t *parts) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t nbig = S.ctl[1];
+    for (uint64_t bi = blockIdx.x; bi < nbig; bi += gridDim.x) {
+        const GBig g = S.big[bi];
+        uint64_t p;
+        uint32_t n, cs, m;
+        gv4_block(P, g.i, p, n);
+        gv4_split_geom(P, S, n, cs, m);
+        const uint32_t L = n - (m - 1u) * cs;
+        const uint32_t per = (m + 63u) / 64u, c0 = t * per, c1 = c0 + per < m ? c0 + per : m;
+        uint32_t s = 0, bytes = 0;
+        for (uint32_t c = c0; c < c1; c++) {
+            const uint32_t len = c + 1u == m ? L : cs;
+            s = gv4_zpow(P.aux, s, len) ^ parts[g.part0 + c];
+            bytes += len;
+        }
+        for (uint32_t off = 1; off < 64u; off <<= 1) {
+            const uint32_t so = (uint32_t)__shfl_down((int)s, off), bo = (uint32_t)__shfl_down((int)bytes, off);
+            if ((t & (2u * off - 1u)) == 0u && t + off < 64u) {
+                s = gv4_zpow(P.aux, s, bo) ^ so;
+                bytes += bo;
+            }
+        }
+        if (t == 0u) {
+            uint32_t st = gv4_zpow(P.aux, ~(P.init ? P.init[g.i] : 0u), n) ^ s;
+            if (P.suffix) st = (st >> 8) ^ P.aux[(st ^ P.suffix[g.i]) & 0xffu];
+            const uint32_t crc = ~st;
+            P.out32[g.i] = (P.flags & 1u) ? mask_crc(crc) : crc;
+        }
+    }
+}
+
+hipError_t launch_gv4_combine(const KParams &P, const GSplit &S, const uint32_t *parts, hipStream_t st) {
+    hipLaunchKernelGGL(gv4_combine_kernel, dim3(1024), dim3(64), 0, st, P, S, parts);
     return hipGetLastError();
 }
 #endif

@@ -199,7 +199,10 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     A.P = P;
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
     A.no_fast = getenv("JL_GV4_NOFAST") ? 1u : 0u;
-    if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0) {
+    // blocks above kGSplitMin (MODE_CRC) are split into chunks folded afterwards
+    const bool can_split = P.mode == jlk::MODE_CRC;
+    if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0 &&
+        !(can_split && P.fixed_bytes > jlk::kGSplitMin)) {
         // every block starts on the 128-B grid: implicit rounds, no pads, no sort
         A.fixed_K = (uint32_t)(P.fixed_bytes / 128);
         JL_HIP(gv4_launch(A, st));
@@ -209,19 +212,36 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     // rounds: ceil(c/8) per bin of c blocks <= n/8 + one partial round per bin (2^17 bins),
     // plus one round per solo block (>= 16 MiB each: at most 18432 in 288 GiB)
     const uint64_t nb = (uint64_t)jlk::kGSoloKey + 1;
-    const uint64_t max_rounds = n / 8 + std::min<uint64_t>(n, nb) + std::min<uint64_t>(n, 18432) + 1;
+    // split blocks: up to part_cap chunks (JL_GV4_PARTCAP: tests), blocks beyond it stay whole
+    const uint64_t part_cap =
+        can_split ? (getenv("JL_GV4_PARTCAP") ? strtoull(getenv("JL_GV4_PARTCAP"), nullptr, 10)
+                                              : std::min<uint64_t>(1ull << 20, 2048 * n))  // <= 2048 chunks a block
+                  : 0;
+    const uint64_t vn = n + part_cap;  // blocks and chunks
+    const uint64_t max_rounds = vn / 8 + std::min<uint64_t>(vn, nb) + std::min<uint64_t>(n, 18432) + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t ab = al((nb + 1) * 4), ad = al(max_rounds * sizeof(jlk::GDesc) * 8);  // hist[nb] = max bin
-    const size_t total = 3 * ab + ad + 256;
+    const size_t a_bb = part_cap ? al(n * 4) : 0, a_big = al((part_cap / 2 + 1) * sizeof(jlk::GBig)),
+                 a_parts = al(part_cap * 4);
+    const size_t total = 3 * ab + ad + 256 + 256 + a_bb + a_big + a_parts;
     char *buf = nullptr;
     if (hipMallocAsync((void **)&buf, total, st) != hipSuccess) return fail(JL_ERR_NOMEM, "gv4 scratch allocation failed");
     uint32_t *hist = (uint32_t *)buf, *cursor = (uint32_t *)(buf + ab), *rstart = (uint32_t *)(buf + 2 * ab);
     jlk::GDesc *desc = (jlk::GDesc *)(buf + 3 * ab);
     uint32_t *n_rounds = (uint32_t *)(buf + 3 * ab + ad);
+    char *sp = buf + 3 * ab + ad + 256;
+    jlk::GSplit SP;
+    SP.ctl = (unsigned long long *)sp;
+    SP.bigbase = (uint32_t *)(sp + 256);
+    SP.big = (jlk::GBig *)(sp + 256 + a_bb);
+    SP.part_cap = (uint32_t)std::min<uint64_t>(part_cap, 0x7fffffffu);
+    uint32_t *parts = (uint32_t *)(sp + 256 + a_bb + a_big);
     hipError_t e = hipMemsetAsync(buf, 0, 2 * ab, st);  // hist, cursor
+    if (e == hipSuccess) e = hipMemsetAsync(SP.ctl, 0, 16, st);
     // null groups of partial rounds: idx = kGNull (the kernel mirrors group 0 there)
     if (e == hipSuccess) e = hipMemsetAsync(desc, 0xff, max_rounds * sizeof(jlk::GDesc) * 8, st);
-    if (e == hipSuccess) e = jlk::launch_gv4_rounds(P, hist, cursor, rstart, desc, n_rounds, st);
+    if (e == hipSuccess) e = jlk::launch_gv4_rounds(P, SP, hist, cursor, rstart, desc, n_rounds, st);
+    A.parts = parts;
     A.desc = desc;
     A.n_rounds = n_rounds;
     unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
@@ -234,6 +254,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
         A.P.dbg = d_dbg;
     }
     if (e == hipSuccess) e = gv4_launch(A, st);
+    if (e == hipSuccess && SP.part_cap) e = jlk::launch_gv4_combine(P, SP, parts, st);
     if (d_dbg) {
         uint32_t hr = 0;
         if (e == hipSuccess) e = hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st);
@@ -262,7 +283,8 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
     // offsets 0.95 vs 1.04 ms), except for small sorted batches, where its ~12
     // pipeline launches cost more than the stream kernel's one;
     // JL_GENERAL=stream / gv4 force either
-    const bool small = P.off && P.n < 4096;
+    // (crc batches always take gv4: a few huge blocks there are split across waves)
+    const bool small = P.off && P.n < 4096 && P.mode != jlk::MODE_CRC;
     const bool want_gv4 = e_g ? !strcmp(e_g, "gv4") : !small;
     if (want_gv4 && gv4_eligible(P)) return run_gv4(P, st);
     if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {

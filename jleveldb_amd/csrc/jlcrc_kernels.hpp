@@ -61,6 +61,24 @@ struct GV4Args {
     uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
     uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
     uint32_t no_fast;           // study (JL_GV4_NOFAST): every ring turn takes the per-entry path
+    uint32_t *parts;            // split blocks: raw chunk states (group idx = kGPart | part index)
+};
+// A block above kGSplitMin (MODE_CRC) is cut into m <= 2048 chunks of S bytes
+// (S a multiple of 128, >= 64 KiB; the last chunk shorter) computed as blocks of
+// their own from state 0, then folded per block by gv4_combine_kernel.
+constexpr uint32_t kGPart = 0x80000000u;
+constexpr uint32_t kAuxZpowDword = 1552;  // must equal jlmath::kAuxZpow (z^(2^k) tables in aux)
+constexpr uint64_t kGSplitMin = 512u << 10;
+struct GBig {        // one split block (gv4_combine_kernel's work item)
+    uint64_t i;      // block index
+    uint32_t part0;  // its first chunk's slot in parts[]
+    uint32_t m;      // chunks
+};
+struct GSplit {       // rounds-pipeline state of the block split
+    uint32_t *bigbase;  // per block: part0, or 0xffffffff (not split)
+    GBig *big;          // split blocks
+    unsigned long long *ctl;  // [0] parts reserved (may exceed part_cap), [1] split blocks
+    uint32_t part_cap;  // parts[] capacity (blocks beyond it stay whole)
 };
 constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
 
@@ -84,8 +102,10 @@ hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream
 template <int MODE>
 hipError_t launch_gv4_m(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st);
 // sorted-pipeline helpers (general_v4.hip, mode-0 object)
-hipError_t launch_gv4_rounds(const KParams &P, uint32_t *hist, uint32_t *cursor, uint32_t *rstart, GDesc *desc,
-                             uint32_t *n_rounds, hipStream_t st);
+hipError_t launch_gv4_rounds(const KParams &P, const GSplit &S, uint32_t *hist, uint32_t *cursor, uint32_t *rstart,
+                             GDesc *desc, uint32_t *n_rounds, hipStream_t st);
+// folds the chunk states of every split block into its result (after the main kernel)
+hipError_t launch_gv4_combine(const KParams &P, const GSplit &S, const uint32_t *parts, hipStream_t st);
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
 template <int MODE>

@@ -152,3 +152,40 @@ def test_gv4_rounds_pipeline_large_bins(gpu, jl, oracle):
     arena = rng.integers(0, 256, pos + 8, dtype=np.uint8)
     got = u32(jl.crc32c_batch_dev(to_dev(arena, gpu), to_dev(offs.view(np.int64), gpu), to_dev(lens.view(np.int32), gpu)))
     assert np.array_equal(got, oracle.batch(arena, offs, lens, threads=THREADS))
+
+
+@pytest.mark.parametrize("part_cap", [None, "8"])
+def test_gv4_split_blocks(gpu, jl, oracle, monkeypatch, part_cap):
+    """Blocks above 512 KiB are split into chunks (computed from state 0 on their
+    own waves) and folded per block with z^len: lengths around the split
+    threshold and the chunk size, an 8 MiB + 77 block, a 40 MiB block (160
+    chunks), unaligned starts, with init / suffix / unmasked variants.
+    part_cap 8: only the first split blocks get chunk slots, the rest stay whole."""
+    if part_cap:
+        monkeypatch.setenv("JL_GV4_PARTCAP", part_cap)
+    rng = np.random.default_rng(25)
+    lens = np.array([(512 << 10) + 1, (512 << 10), 600 << 10, (1 << 20) + 3, (768 << 10), (8 << 20) + 77, 40 << 20,
+                     5, 4096, 0, (256 << 10) * 3 - 1], np.uint32)
+    offs = np.zeros(lens.size, np.uint64)
+    pos = 0
+    for i in range(lens.size):
+        pos += int(rng.integers(0, 200))
+        offs[i] = pos
+        pos += int(lens[i])
+    arena = rng.integers(0, 256, pos + 8, dtype=np.uint8)
+    d = (to_dev(arena, gpu), to_dev(offs.view(np.int64), gpu), to_dev(lens.view(np.int32), gpu))
+    assert np.array_equal(u32(jl.crc32c_batch_dev(*d)), oracle.batch(arena, offs, lens, threads=THREADS))
+    init = rng.integers(0, 2**32, lens.size, dtype=np.uint64).astype(np.uint32)
+    sfx = rng.integers(0, 256, lens.size, dtype=np.uint8)
+    got = u32(jl.crc32c_batch_dev(*d, init=to_dev(init.view(np.int32), gpu), suffix=to_dev(sfx, gpu), flags=0))
+    assert np.array_equal(got, oracle.batch(arena, offs, lens, init=init, suffix=sfx, flags=0, threads=THREADS))
+
+
+@pytest.mark.parametrize("block_bytes", [(1 << 20), (3 << 20) + 5])
+def test_gv4_split_fixed_stride(gpu, jl, oracle, block_bytes):
+    """Few large fixed-stride blocks (the crc32c_fixed_dev path) go through the split."""
+    rng = np.random.default_rng(block_bytes)
+    n = 9
+    host = rng.integers(0, 256, n * block_bytes, dtype=np.uint8)
+    got = u32(jl.crc32c_fixed_dev(to_dev(host, gpu), block_bytes, n))
+    assert np.array_equal(got, oracle.fixed(host, block_bytes, n, threads=THREADS))

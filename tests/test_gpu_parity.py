@@ -115,6 +115,7 @@ def test_batch_every_length_and_alignment(gpu, jl, oracle):
 @pytest.mark.parametrize("depth,partition", [("32", True), ("48", False), ("16", False)])
 def test_stream_depths_and_partition(gpu, jl, oracle, monkeypatch, depth, partition):
     """Stream-kernel ring depths (JL_STREAM_DEPTH) and the count split (JL_NO_PARTITION)."""
+    monkeypatch.setenv("JL_GENERAL", "stream")
     monkeypatch.setenv("JL_STREAM_DEPTH", depth)
     if not partition:
         monkeypatch.setenv("JL_NO_PARTITION", "1")
