@@ -54,7 +54,7 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
 // the 8 ring slots: (slot, register quad, its 4 registers), pinned in v224..v255
 #define JL_GV4_RING 8
-#define JL_GV4_VGPR_BUDGET 224
+#define JL_GV4_VGPR_BUDGET 216  // v216..v223: the two round-descriptor sets, v224..v255: the ring
 #define JL_GV4_SLOTS(X) \
     X(0, "v[224:227]", "v224", "v225", "v226", "v227") \
     X(1, "v[228:231]", "v228", "v229", "v230", "v231") \
@@ -128,6 +128,42 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
     return v;
 }
 
+// Round descriptors prefetched with a VECTOR load into one of two pinned register
+// sets (v216..v219 / v220..v223, each lane its group's 16-B GDesc), touched only
+// by inline asm like the ring.  The prefetch cursor issues round k+1's load when
+// it starts round k, if round k has >= P entries: the ring's own waits then
+// cover it before either cursor reads it (at least P-1 younger ring loads), and
+// the extra load only makes those waits stricter.  Otherwise (short rounds,
+// first round) the scalar-load round_view is used.  r1: the scalar loads'
+// latency was ~3.6 us per round and wave (1M x 4 KiB through descriptors 0.89
+// vs 0.66 ms without any).
+__device__ __forceinline__ void desc_issue(const GV4Args &A, uint64_t r, uint32_t q, uint32_t set) {
+    const uint64_t a = (uint64_t)(uintptr_t)(A.desc + r * 8u + q);
+    if (set)
+        asm volatile("global_load_dwordx4 v[220:223], %0, off" ::"v"(a) : "memory", "v220", "v221", "v222", "v223");
+    else
+        asm volatile("global_load_dwordx4 v[216:219], %0, off" ::"v"(a) : "memory", "v216", "v217", "v218", "v219");
+}
+__device__ __forceinline__ RoundView desc_read(uint32_t set) {
+    uint32_t lo, hi, ix, k;
+    if (set)
+        asm volatile("v_mov_b32 %0, v220\n\tv_mov_b32 %1, v221\n\tv_mov_b32 %2, v222\n\tv_mov_b32 %3, v223"
+                     : "=v"(lo), "=v"(hi), "=v"(ix), "=v"(k));
+    else
+        asm volatile("v_mov_b32 %0, v216\n\tv_mov_b32 %1, v217\n\tv_mov_b32 %2, v218\n\tv_mov_b32 %3, v219"
+                     : "=v"(lo), "=v"(hi), "=v"(ix), "=v"(k));
+    // empty groups of a partial round mirror group 0 (lane 0)
+    const bool nul = ix == kGNull;
+    lo = nul ? (uint32_t)__builtin_amdgcn_readlane((int)lo, 0) : lo;
+    hi = nul ? (uint32_t)__builtin_amdgcn_readlane((int)hi, 0) : hi;
+    RoundView v;
+    v.p = ((uint64_t)(hi & 0xffffffu) << 32) | lo;
+    v.d = hi >> 24;
+    v.idx = ix;
+    v.K = (uint32_t)__builtin_amdgcn_readlane((int)k, 0);
+    return v;
+}
+
 template <int MODE>
 __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
     const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
@@ -140,21 +176,37 @@ template <int MODE>
 struct GPF {
     uint64_t r, R, W;
     uint32_t e, E, K;
+    uint32_t k;      // sequence number of the current round (descriptor set k & 1)
+    bool vec_next;   // the next round's descriptor was issued into set (k+1) & 1
+    uint32_t Eprev;  // entries of round k-1
     uint64_t addr;        // per lane: next step's chunk address
     uint64_t side_addr;   // per lane: the side chunk
     uint64_t dummy;       // a mapped address (zero page) for lanes with nothing to load
 
-    __device__ __forceinline__ void setup(const GV4Args &A, uint32_t lane) {
+    __device__ __forceinline__ void setup(const GV4Args &A, uint32_t lane, bool vec) {
         const uint32_t q = lane >> 3, l = lane & 7u;  // group, lane in group
         RoundView v;
-        for (;;) {  // K == 0 rounds (empty blocks, results already written) are skipped
-            v = round_view(A, r, q);
-            if (uni(v.K) != 0u) break;
-            r = uni64(r + W);
-            if (r >= R) return;
+        if (vec) {
+            v = desc_read(k & 1u);
+        } else {
+            for (;;) {  // K == 0 rounds (empty blocks, results already written) are skipped
+                v = round_view(A, r, q);
+                if (uni(v.K) != 0u) break;
+                r = uni64(r + W);
+                if (r >= R) return;
+            }
         }
         K = uni(v.K);
+        Eprev = E;
         E = uni(n_entries<MODE>(A, K));
+        // issue round k+1's descriptor into set (k+1) & 1 = (k-1) & 1 when
+        //  * E_k > P: >= P-2 ring loads are issued behind it before either cursor
+        //    reads it (and none of round 0's P priming loads reaches round 1), and
+        //  * E_{k-1} >= P: the compute cursor has already read round k-1's
+        //    descriptor from that set (it is P entries behind)
+        // gv4 finish() takes the same decision from the same E values
+        vec_next = A.desc && E > (uint32_t)JL_GV4_RING && (k == 0u || Eprev >= (uint32_t)JL_GV4_RING) && r + W < R;
+        if (vec_next) desc_issue(A, r + W, q, (k + 1u) & 1u);
         const uint64_t p = v.p, n = (uint64_t)K * 128u - (p & 127u) - v.d;
         const uint64_t pa = p & ~(uint64_t)15;
         addr = (p & ~(uint64_t)127) + 16u * l;
@@ -178,7 +230,10 @@ struct GPF {
         W = waves;
         R = nr;
         dummy = dmy;
-        if (r < R) setup(A, lane);
+        k = 0;
+        E = 0;
+        vec_next = false;
+        if (r < R) setup(A, lane, false);
     }
     // Address of the next entry (advancing the cursor).  The ring load itself is
     // issued by the caller at ONE site per slot: a load asm in several branches
@@ -214,7 +269,8 @@ struct GPF {
         }
         if (++e == E) {
             r += W;
-            if (r < R) setup(A, lane);
+            k++;
+            if (r < R) setup(A, lane, vec_next);
             r = uni64(r);
         }
         e = uni(e);
@@ -251,8 +307,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
 
     GPF<MODE> pf;
     pf.init(A, cr, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
-    // The ring lives in PINNED registers v192..v255 (slot u = v[192+4u : 195+4u]),
-    // above the compiler's budget (amdgpu_num_vgpr(192)): the register allocator
+    // The ring lives in PINNED registers v224..v255 (slot u = v[224+4u : 227+4u]),
+    // above the compiler's budget (amdgpu_num_vgpr(216); v216..v223 hold the two
+    // prefetched round-descriptor sets): the register allocator
     // can never copy, reuse or spill a slot while its load is in flight — with
     // compiler-allocated ring values this kernel's branchy rounds made it do that
     // (r1: intermittent faults).  Each slot is touched only by inline asm: the
@@ -274,7 +331,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     JL_GV4_SLOTS(JL_PRIME)
 #undef JL_PRIME
 
-    uint32_t cK = uni(cv.K), cE = uni(n_entries<MODE>(A, cK)), ce = 0;
+    uint32_t cK = uni(cv.K), cE = uni(n_entries<MODE>(A, cK)), ce = 0, ck = 0, cEprev = 0;
     v4u side_c;  // lane 0 / 1 of each group: the side chunk
     uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;
 
@@ -387,12 +444,23 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
                 A.P.out8[cv.idx] = stored == m ? 1u : 0u;
             }
         }
-        // next round of the compute cursor (skipping K == 0 rounds)
-        for (;;) {
+        // next round of the compute cursor: from the descriptor set the prefetch
+        // cursor loaded if the finished round had >= P entries, else scalar loads
+        // (skipping K == 0 rounds)
+        const bool vec = A.desc && cE > (uint32_t)P_ && (ck == 0u || cEprev >= (uint32_t)P_);  // as GPF::setup
+        cEprev = cE;
+        ck++;
+        if (vec) {
             cr = uni64(cr + waves);
             if (cr >= R) return false;
-            cv = round_view(A, cr, q);
-            if (uni(cv.K) != 0u) break;
+            cv = desc_read(ck & 1u);
+        } else {
+            for (;;) {
+                cr = uni64(cr + waves);
+                if (cr >= R) return false;
+                cv = round_view(A, cr, q);
+                if (uni(cv.K) != 0u) break;
+            }
         }
         cK = uni(cv.K);
         cE = uni(n_entries<MODE>(A, cK));

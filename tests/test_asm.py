@@ -54,7 +54,7 @@ def test_no_stale_ring_reads(asm):
 
     def one(s, b):
         if "crc_gv4_kernel" in s:
-            return check_pinned(b) + check_local(b)
+            return check_pinned(b, first=216) + check_local(b)
         return check_local(b) if any(k in s for k in branchy) else check(b)
 
     problems = {s: one(s, b) for s, b in ks.items()}
