@@ -67,7 +67,7 @@ struct Context {
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
     // staging workspace (host-memory APIs, log verify)
-    DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp;
+    DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp, ws_slot;
     // streaming pipeline (jl_crc32c_fixed): two slots, each a device chunk + result
     // buffer, a pinned staging buffer (pageable sources) and its own stream
     struct Slot {
@@ -388,7 +388,7 @@ int jl_shutdown(void) {
     (void)hipSetDevice(c.device);
     (void)hipStreamSynchronize(c.stream);
     for (DevBuf *b : {&c.ws_data, &c.ws_off, &c.ws_len, &c.ws_init, &c.ws_sfx, &c.ws_out, &c.ws_cnt, &c.ws_start,
-                      &c.ws_ev, &c.ws_ok, &c.ws_tmp})
+                      &c.ws_ev, &c.ws_ok, &c.ws_tmp, &c.ws_slot})
         b->release();
     for (auto &sl : c.slot) {
         sl.d_in.release();
@@ -657,8 +657,11 @@ static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, 
     if (nb == 0) return JL_OK;
     JL_HIP(c.ws_cnt.ensure(nb * 8));
     JL_HIP(c.ws_start.ensure(nb * 8));
+    JL_HIP(c.ws_slot.ensure(nb * jlk::kLogSlots * sizeof(jlk::LogSlot)));
     uint64_t *cnt = (uint64_t *)c.ws_cnt.p, *start = (uint64_t *)c.ws_start.p;
-    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 0, cnt, nullptr, nullptr, nullptr, nullptr, st));
+    jlk::LogSlot *slots = (jlk::LogSlot *)c.ws_slot.p;
+    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 0, cnt, nullptr, nullptr, nullptr, nullptr, slots,
+                                st));
     size_t tmp = 0;
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, start, (int)nb, st));
     JL_HIP(c.ws_tmp.ensure(tmp));
@@ -675,7 +678,7 @@ static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, 
     JL_HIP(c.ws_len.ensure(total * 4));
     JL_HIP(c.ws_ok.ensure(total));
     JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 1, cnt, start, (jlk::LogEvent *)d_events,
-                                (uint64_t *)c.ws_off.p, (uint32_t *)c.ws_len.p, st));
+                                (uint64_t *)c.ws_off.p, (uint32_t *)c.ws_len.p, slots, st));
     if (checksum) {
         jlk::KParams P = base_params(d_log, total, jlk::MODE_LOG_VERIFY);
         P.off = (const uint64_t *)c.ws_off.p;

@@ -516,11 +516,30 @@ __global__ __launch_bounds__(1024) void crc_general_kernel(const uint4 *__restri
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
+__device__ __forceinline__ void log_put(LogEvent *ev, uint64_t *d_off, uint32_t *d_len, uint64_t at, uint64_t p,
+                                        uint32_t length, uint32_t type, uint8_t kind) {
+    LogEvent e;
+    e.offset = p;
+    e.length = length;
+    e.type = (uint8_t)type;
+    e.kind = kind;
+    e.pad = 0;
+    ev[at] = e;
+    if (kind == 1) { d_off[at] = p + 6; d_len[at] = 1u + length; }
+    else { d_off[at] = p; d_len[at] = 0; }
+}
+
+// With slots (r1): pass 0 also keeps each block's first kLogSlots decisions
+// (8 B each), log_expand_kernel writes them out one thread per event, and pass 1
+// only re-walks the blocks with more events than that.  Without slots pass 1
+// re-walks every block (the walk is a chain of dependent header loads).
 __global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, uint64_t n_blocks, int pass,
                                 uint64_t *__restrict__ counts, const uint64_t *__restrict__ starts,
-                                LogEvent *__restrict__ ev, uint64_t *__restrict__ d_off, uint32_t *__restrict__ d_len) {
+                                LogEvent *__restrict__ ev, uint64_t *__restrict__ d_off, uint32_t *__restrict__ d_len,
+                                LogSlot *__restrict__ slots) {
     uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= n_blocks) return;
+    if (pass && slots && counts[b] <= kLogSlots) return;  // written by log_expand_kernel
     const uint64_t bs = b * 32768u;
     const uint64_t be = (bs + 32768u < size) ? bs + 32768u : size;
     const bool eof = (be - bs) < 32768u;
@@ -543,21 +562,31 @@ __global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, 
             else kind = 1;
         }
         if (pass) {
-            LogEvent e;
-            e.offset = p;
-            e.length = length;
-            e.type = (uint8_t)type;
-            e.kind = kind;
-            e.pad = 0;
-            ev[o + cnt] = e;
-            if (kind == 1) { d_off[o + cnt] = p + 6; d_len[o + cnt] = 1u + length; }
-            else { d_off[o + cnt] = p; d_len[o + cnt] = 0; }
+            if (!slots || cnt >= kLogSlots) log_put(ev, d_off, d_len, o + cnt, p, length, type, kind);
+        } else if (slots && cnt < kLogSlots) {
+            LogSlot sl;
+            sl.off = (uint16_t)(p - bs);
+            sl.length = (uint16_t)length;
+            sl.type = (uint8_t)type;
+            sl.kind = kind;
+            sl.pad = 0;
+            slots[b * kLogSlots + cnt] = sl;
         }
         cnt++;
         if (stop) break;
         p += 7u + length;
     }
     if (!pass) counts[b] = cnt;
+}
+
+__global__ void log_expand_kernel(uint64_t n_blocks, const uint64_t *__restrict__ counts,
+                                  const uint64_t *__restrict__ starts, const LogSlot *__restrict__ slots,
+                                  LogEvent *__restrict__ ev, uint64_t *__restrict__ d_off, uint32_t *__restrict__ d_len) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t b = t / kLogSlots, j = t % kLogSlots;
+    if (b >= n_blocks || j >= counts[b]) return;
+    const LogSlot sl = slots[t];
+    log_put(ev, d_off, d_len, starts[b] + j, b * 32768u + sl.off, sl.length, sl.type, sl.kind);
 }
 
 // Applies the per-record CRC results (ok[i] = 1 match) and truncates each block
@@ -739,10 +768,14 @@ hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part
 }
 
 hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
-                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st) {
+                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, LogSlot *slots,
+                           hipStream_t st) {
     unsigned grid = (unsigned)((n_blocks + 255) / 256);
+    if (pass && slots)
+        hipLaunchKernelGGL(log_expand_kernel, dim3((unsigned)((n_blocks * kLogSlots + 255) / 256)), dim3(256), 0, st,
+                           n_blocks, counts, starts, slots, ev, d_off, d_len);
     hipLaunchKernelGGL(log_walk_kernel, dim3(grid), dim3(256), 0, st, log, size, n_blocks, pass, counts, starts, ev,
-                       d_off, d_len);
+                       d_off, d_len, slots);
     return hipGetLastError();
 }
 

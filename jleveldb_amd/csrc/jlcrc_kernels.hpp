@@ -110,8 +110,19 @@ hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
 template <int MODE>
 hipError_t launch_stream_m(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
+// log walk: pass 0 counts events per 32 KiB block (and keeps the first kLogSlots
+// decisions of each in `slots` when given), pass 1 writes them (slots: expand +
+// re-walk of the blocks with more events)
+constexpr uint64_t kLogSlots = 64;
+struct LogSlot {
+    uint16_t off;     // header offset in the block
+    uint16_t length;
+    uint8_t type, kind;
+    uint16_t pad;
+};
 hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
-                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, hipStream_t st);
+                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, LogSlot *slots,
+                           hipStream_t st);
 // Byte-balanced partition of n blocks over `parts` waves for the stream kernel:
 // incl[i] = sum of weights of blocks 0..i (weight = len + per-block overhead);
 // part[w] = first block of wave w (part[0] = 0, part[parts] = n).

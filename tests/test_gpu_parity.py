@@ -375,3 +375,19 @@ def test_log_emit_dev_matches_logwriter(gpu, jl, oracle, dest_length):
     if dest_length == 0:
         recs, reps = jl.log_read_records(got)
         assert reps == [] and [r[1] for r in recs] == payloads
+
+
+def test_log_many_small_records(gpu, jl, oracle):
+    """Blocks with far more than 64 physical records (the walk keeps the first 64
+    decisions of a block and re-walks the rest) next to blocks with fewer, with
+    bit flips; device-resident and host entry points."""
+    rng = np.random.default_rng(31)
+    sizes = np.concatenate([rng.integers(0, 40, 4000), rng.integers(500, 3000, 60), rng.integers(0, 9, 3000)])
+    payloads = [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+    log = bytearray(oracle.log_write(payloads))
+    for _ in range(6):
+        log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
+    log = bytes(log)
+    want = _events(oracle.log_events(log, True))
+    assert _events(jl.log_verify(log, True)) == want
+    assert jl.log_read_records(log, True) == oracle.log_read(log, True)
