@@ -64,6 +64,17 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     X(5, "v[244:247]", "v244", "v245", "v246", "v247") \
     X(6, "v[248:251]", "v248", "v249", "v250", "v251") \
     X(7, "v[252:255]", "v252", "v253", "v254", "v255")
+// the two half turns (slots 0..3 and 4..7)
+#define JL_GV4_SLOTS_LO(X) \
+    X(0, "v[224:227]", "v224", "v225", "v226", "v227") \
+    X(1, "v[228:231]", "v228", "v229", "v230", "v231") \
+    X(2, "v[232:235]", "v232", "v233", "v234", "v235") \
+    X(3, "v[236:239]", "v236", "v237", "v238", "v239")
+#define JL_GV4_SLOTS_HI(X) \
+    X(4, "v[240:243]", "v240", "v241", "v242", "v243") \
+    X(5, "v[244:247]", "v244", "v245", "v246", "v247") \
+    X(6, "v[248:251]", "v248", "v249", "v250", "v251") \
+    X(7, "v[252:255]", "v252", "v253", "v254", "v255")
 
 template <int MODE>
 struct GV4 {
@@ -506,29 +517,50 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         if (++ce == cE && !finish()) break;                                                                \
         JL_LOAD(RQ, R0, R1, R2, R3)                                                                        \
     }
-    // Fast turn: the next P entries of BOTH cursors are plain steps of their
-    // current rounds (no rare entry, no epilogue, no round switch), so the turn
-    // is straight-line code: wait, the 4 chains, and the refill at the cursor's
-    // address + 128 u — no per-step bookkeeping.  Any other turn takes the
-    // general per-step path below (it always ends back on slot 0).
+    // Fast half turn: the next 4 entries of BOTH cursors are plain steps of their
+    // current rounds (no rare entry, no epilogue, no round switch), so they run
+    // as straight-line code: wait, the 4 chains, and the refill at the cursor's
+    // address + 128 (u mod 4) — no per-step bookkeeping.  Otherwise the half
+    // takes the per-entry path (either way it ends on the next half's slot).
+    // Half turns rather than whole 8-entry turns: a round boundary then blocks
+    // fewer entries from the fast path (rounds of 32 entries: ~72 % fast vs ~47 %).
 #define JL_F(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
         JL_XS4(R0, R1, R2, R3)                                                                             \
-        JL_GLD(RQ, pf.addr, 128 * (u), R0, R1, R2, R3)                                                     \
+        JL_GLD(RQ, pf.addr, 128 * ((u) & 3), R0, R1, R2, R3)                                               \
     }
     const bool fast_ok = !A.P.dbg && !A.no_fast;
-    for (;;) {
-        if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
-            pf.e + (uint32_t)P_ < pf.E) {
-            JL_GV4_SLOTS(JL_F)
-            ce = uni(ce + (uint32_t)P_);
-            pf.e = uni(pf.e + (uint32_t)P_);
-            pf.addr += 128u * P_;
-            continue;
-        }
-        JL_GV4_SLOTS(JL_G)
+#define JL_HALF(SLOTS)                                                                                     \
+    if (fast_ok && ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E) {             \
+        SLOTS(JL_F)                                                                                        \
+        ce = uni(ce + 4u);                                                                                 \
+        pf.e = uni(pf.e + 4u);                                                                             \
+        pf.addr += 512u;                                                                                   \
+    } else {                                                                                               \
+        SLOTS(JL_G)                                                                                        \
     }
+    if constexpr (VAR == 3) {  // study: whole 8-entry fast turns only
+        for (;;) {
+            if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
+                pf.e + (uint32_t)P_ < pf.E) {
+                JL_GV4_SLOTS_LO(JL_F)
+                pf.addr += 512u;
+                JL_GV4_SLOTS_HI(JL_F)
+                ce = uni(ce + (uint32_t)P_);
+                pf.e = uni(pf.e + (uint32_t)P_);
+                pf.addr += 512u;
+                continue;
+            }
+            JL_GV4_SLOTS(JL_G)
+        }
+    } else {
+        for (;;) {
+            JL_HALF(JL_GV4_SLOTS_LO)
+            JL_HALF(JL_GV4_SLOTS_HI)
+        }
+    }
+#undef JL_HALF
 #undef JL_F
 #undef JL_G
 #undef JL_XS4
@@ -546,6 +578,9 @@ template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
     if (getenv("JL_GV4_STRICT"))  // debugging: vmcnt(0) before every ring use
         hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+                           zero);
+    else if (getenv("JL_GV4_FULLTURN"))  // study: whole 8-entry fast turns only
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
                            zero);
     else if (getenv("JL_GV4_NONT"))  // study: ring loads without the nt cache policy
         hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,

@@ -39,11 +39,13 @@ res = {}
 big = 8 << 20
 nbig = arena.numel() // big
 for rnd in range(2):
-    for v in ["", "nofast"]:
-        if v:
+    for v in ["", "nofast", "fullturn"]:
+        os.environ.pop("JL_GV4_NOFAST", None)
+        os.environ.pop("JL_GV4_FULLTURN", None)
+        if v == "nofast":
             os.environ["JL_GV4_NOFAST"] = "1"
-        else:
-            os.environ.pop("JL_GV4_NOFAST", None)
+        if v == "fullturn":
+            os.environ["JL_GV4_FULLTURN"] = "1"
         a = t_of(lambda: jl.crc32c_batch_dev(arena, off, ln, out=out))
         b = t_of(lambda: jl.crc32c_fixed_dev(arena, 1024, n, out=out))
         c = t_of(lambda: jl.crc32c_fixed_dev(arena, big, nbig, out=out))

@@ -56,13 +56,14 @@ out2 = torch.empty(n2, dtype=torch.int32, device=dev)
 
 
 def setv(v):
-    os.environ["JL_GENERAL"] = v if v in ("chunk", "gv4") else ("gv4" if v == "gv4nont" else "stream")
-    if v == "gv4nont":
-        os.environ["JL_GV4_NONT"] = "1"
-    else:
-        os.environ.pop("JL_GV4_NONT", None)
+    os.environ["JL_GENERAL"] = v if v in ("chunk", "gv4") else ("gv4" if v.startswith("gv4") else "stream")
+    for knob, name in (("JL_GV4_NONT", "gv4nont"), ("JL_GV4_FULLTURN", "gv4full")):
+        if v == name:
+            os.environ[knob] = "1"
+        else:
+            os.environ.pop(knob, None)
     os.environ.pop("JL_NO_PARTITION", None)
-    if v not in ("chunk", "gv4", "gv4nont"):
+    if v not in ("chunk",) and not v.startswith("gv4"):
         os.environ["JL_STREAM_DEPTH"] = v[1:].replace("np", "")
         if v.endswith("np"):
             os.environ["JL_NO_PARTITION"] = "1"
