@@ -183,7 +183,7 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 
 
 // Prefetch cursor: walks the wave's rounds r = w, w+W, ... entry by entry.
-template <int MODE>
+template <int MODE, bool DBG>
 struct GPF {
     uint64_t r, R, W;
     uint32_t e, E, K;
@@ -252,7 +252,7 @@ struct GPF {
     // allocator may resolve that phi with a copy of the still-in-flight register.
     __device__ __forceinline__ uint64_t next(const GV4Args &A, uint32_t lane) {
         const uint64_t a = next_raw(A, lane);
-        if (A.P.dbg) {  // debugging (JL_GV4_DEBUG): log and neutralise loads outside the valid range
+        if (DBG && A.P.dbg) {  // debugging (JL_GV4_DEBUG): log and neutralise loads outside the valid range
             const uint64_t zp = dummy - 16u * lane;
             if (!((a >= A.P.dbg_lo && a + 16 <= A.P.dbg_hi) || (a >= zp && a + 16 <= zp + 4096))) {
                 const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
@@ -290,11 +290,13 @@ struct GPF {
 };
 
 // VAR: 0 = default (nt ring loads), 1 = strict (vmcnt(0) before every ring use:
-// debugging), 2 = ring loads without nt (cache-policy study)
+// debugging), 2 = ring loads without nt (cache-policy study), 3 = whole 8-entry
+// fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study)
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_GV4_VGPR_BUDGET))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
     constexpr int P_ = JL_GV4_RING;
+    constexpr bool DBG = VAR == 4;  // JL_GV4_DEBUG builds the address checks in
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     uint32_t zero_v;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
 
-    GPF<MODE> pf;
+    GPF<MODE, DBG> pf;
     pf.init(A, cr, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
     // The ring lives in PINNED registers v224..v255 (slot u = v[224+4u : 227+4u]),
     // above the compiler's budget (amdgpu_num_vgpr(216); v216..v223 hold the two
@@ -429,7 +431,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
             st = (st >> 8) ^ lds_at(lds, kG4T0Byte + (((st ^ sfx) & 0xffu) << 2));
         }
         const uint32_t crc = ~st, m = mask_crc(crc);
-        if (A.P.dbg && l == 0u && cv.idx < kGPart && cv.idx >= A.P.n) {
+        if (DBG && A.P.dbg && l == 0u && cv.idx < kGPart && cv.idx >= A.P.n) {
             const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
             if (slot < 256) {
                 A.P.dbg[1 + 4 * slot] = cr;
@@ -530,7 +532,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         JL_XS4(R0, R1, R2, R3)                                                                             \
         JL_GLD(RQ, pf.addr, 128 * ((u) & 3), R0, R1, R2, R3)                                               \
     }
-    const bool fast_ok = !A.P.dbg && !A.no_fast;
+    const bool fast_ok = !DBG && VAR != 5;  // debugging / study variants: per-entry path only
 #define JL_HALF(SLOTS)                                                                                     \
     if (fast_ok && ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E) {             \
         SLOTS(JL_F)                                                                                        \
@@ -578,6 +580,12 @@ template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
     if (getenv("JL_GV4_STRICT"))  // debugging: vmcnt(0) before every ring use
         hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+                           zero);
+    else if (A.P.dbg)  // JL_GV4_DEBUG: address range checks
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 4>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
+                           zero);
+    else if (A.no_fast)  // study: per-entry path only
+        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 5>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
                            zero);
     else if (getenv("JL_GV4_FULLTURN"))  // study: whole 8-entry fast turns only
         hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
