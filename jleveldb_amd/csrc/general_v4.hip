@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t sel8(uint32_t q, uint32_t a0, uint32_t a1, u
     return lo;
 }
 
-__device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, uint32_t q) {
+__device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, uint32_t q) {
     RoundView v;
     if (A.desc) {
         // the round's 8 descriptors (128 B) with two scalar loads: SMEM/lgkmcnt, so the
@@ -106,7 +106,7 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
         // reads (r1: s[16:31] <- [s[16:17]] then [s[16:17] + 64] read a returned
         // descriptor word as the address when the wave was descheduled in between)
         typedef uint32_t v16u __attribute__((ext_vector_type(16)));
-        const uint64_t ga = uni64((uint64_t)(uintptr_t)(A.desc + r * 8u));
+        const uint64_t ga = uni64((uint64_t)(uintptr_t)(A.desc + (uint64_t)r * 8u));
         v16u d0, d1;
         asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
                      : "=&s"(d0), "=&s"(d1) : "s"(ga) : "memory");
@@ -129,8 +129,8 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
         v.d = hi >> 24;
         v.idx = sel8(q, ix[0], ix[1], ix[2], ix[3], ix[4], ix[5], ix[6], ix[7]);
     } else {  // 128-B aligned base and stride (run_gv4): f = d = 0
-        const uint64_t i = uni64(r) * 8u + q;
-        const uint64_t ie = i < A.P.n ? i : uni64(r) * 8u;
+        const uint64_t i = (uint64_t)uni(r) * 8u + q;
+        const uint64_t ie = i < A.P.n ? i : (uint64_t)uni(r) * 8u;
         v.K = A.fixed_K;
         v.d = 0;
         v.p = (uint64_t)(uintptr_t)A.P.base + ie * A.P.fixed_bytes;
@@ -148,8 +148,8 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint64_t r, ui
 // first round) the scalar-load round_view is used.  r1: the scalar loads'
 // latency was ~3.6 us per round and wave (1M x 4 KiB through descriptors 0.89
 // vs 0.66 ms without any).
-__device__ __forceinline__ void desc_issue(const GV4Args &A, uint64_t r, uint32_t q, uint32_t set) {
-    const uint64_t a = (uint64_t)(uintptr_t)(A.desc + r * 8u + q);
+__device__ __forceinline__ void desc_issue(const GV4Args &A, uint32_t r, uint32_t q, uint32_t set) {
+    const uint64_t a = (uint64_t)(uintptr_t)(A.desc + (uint64_t)r * 8u + q);
     if (set)
         asm volatile("global_load_dwordx4 v[220:223], %0, off" ::"v"(a) : "memory", "v220", "v221", "v222", "v223");
     else
@@ -185,7 +185,7 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 // Prefetch cursor: walks the wave's rounds r = w, w+W, ... entry by entry.
 template <int MODE, bool DBG>
 struct GPF {
-    uint64_t r, R, W;
+    uint32_t r, R, W;  // rounds (< 2^31)
     uint32_t e, E, K;
     uint32_t k;      // sequence number of the current round (descriptor set k & 1)
     bool vec_next;   // the next round's descriptor was issued into set (k+1) & 1
@@ -203,7 +203,7 @@ struct GPF {
             for (;;) {  // K == 0 rounds (empty blocks, results already written) are skipped
                 v = round_view(A, r, q);
                 if (uni(v.K) != 0u) break;
-                r = uni64(r + W);
+                r = uni(r + W);
                 if (r >= R) return;
             }
         }
@@ -235,7 +235,7 @@ struct GPF {
         side_addr = l == 0u ? c0 : (l == 1u ? c1 : dummy);
         e = 0;
     }
-    __device__ __forceinline__ void init(const GV4Args &A, uint64_t w, uint64_t waves, uint64_t nr, uint32_t lane,
+    __device__ __forceinline__ void init(const GV4Args &A, uint32_t w, uint32_t waves, uint32_t nr, uint32_t lane,
                                          uint64_t dmy) {
         r = w;
         W = waves;
@@ -282,7 +282,7 @@ struct GPF {
             r += W;
             k++;
             if (r < R) setup(A, lane, vec_next);
-            r = uni64(r);
+            r = uni(r);
         }
         e = uni(e);
         return a;
@@ -301,17 +301,17 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
     load_image(lds, img);
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
     const GLanes gl(lane);
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t w = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    const uint64_t R = A.desc ? (uint64_t)*A.n_rounds : (A.P.n + 7u) / 8u;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t w = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    const uint32_t R = A.desc ? *A.n_rounds : (uint32_t)((A.P.n + 7u) / 8u);  // rounds < 2^31
     // compute cursor: the wave's first round with K > 0
-    uint64_t cr = w;
+    uint32_t cr = w;
     RoundView cv;
     for (;;) {
         if (cr >= R) return;
         cv = round_view(A, cr, q);
         if (uni(cv.K) != 0u) break;
-        cr = uni64(cr + waves);
+        cr = uni(cr + waves);
     }
     const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
     const uint32_t e0 = side ? 1u : 0u;
@@ -464,12 +464,12 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
         cEprev = cE;
         ck++;
         if (vec) {
-            cr = uni64(cr + waves);
+            cr = uni(cr + waves);
             if (cr >= R) return false;
             cv = desc_read(ck & 1u);
         } else {
             for (;;) {
-                cr = uni64(cr + waves);
+                cr = uni(cr + waves);
                 if (cr >= R) return false;
                 cv = round_view(A, cr, q);
                 if (uni(cv.K) != 0u) break;
