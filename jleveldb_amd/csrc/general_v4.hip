@@ -762,7 +762,15 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uin
 
 // hist[kGSoloKey + 1] holds the largest non-solo bin (atomicMax in the hist kernel):
 // the scan only walks [0, that], in coalesced tiles of 4096 bins through LDS
-__global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, uint32_t *rstart, uint32_t *n_rounds) {
+// The scan also marks the empty groups of every bin's last, partial round
+// (idx = kGNull; the main kernel mirrors group 0 there) and groups 1..7 of the
+// solo rounds, so the descriptor table needs no clearing.
+__device__ __forceinline__ void gv4_null_groups(GDesc *desc, uint64_t round, uint32_t from) {
+    for (uint32_t g = from; g < 8u; g++) desc[round * 8u + g].idx = kGNull;
+}
+
+__global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, uint32_t *rstart, uint32_t *n_rounds,
+                                                        GDesc *desc) {
     __shared__ uint32_t tile[4096];
     __shared__ uint32_t part[1024];
     const uint32_t t = threadIdx.x;
@@ -786,10 +794,13 @@ __global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, ui
         }
         const uint32_t ex = carry + part[t] - sum;
         const uint32_t b = t0 + 4 * t;
-        if (b < nbins) rstart[b] = ex;
-        if (b + 1 < nbins) rstart[b + 1] = ex + r0;
-        if (b + 2 < nbins) rstart[b + 2] = ex + r0 + r1;
-        if (b + 3 < nbins) rstart[b + 3] = ex + r0 + r1 + r2;
+        const uint32_t st4[4] = {ex, ex + r0, ex + r0 + r1, ex + r0 + r1 + r2};
+        for (uint32_t j = 0; j < 4u; j++) {
+            if (b + j >= nbins) break;
+            rstart[b + j] = st4[j];
+            const uint32_t c = hist[b + j];
+            if (c & 7u) gv4_null_groups(desc, (uint64_t)st4[j] + c / 8u, c & 7u);
+        }
         carry += part[1023];
         __syncthreads();  // part / tile reused by the next tile
     }
@@ -797,6 +808,7 @@ __global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, ui
         rstart[kGSoloKey] = carry;
         *n_rounds = carry + hist[kGSoloKey];
     }
+    for (uint32_t j = t; j < hist[kGSoloKey]; j += 1024u) gv4_null_groups(desc, (uint64_t)carry + j, 1u);
 }
 
 __device__ __forceinline__ void gv4_put(GDesc *desc, const uint32_t *rstart, uint32_t b, uint32_t r, uint64_t p,
@@ -871,7 +883,7 @@ hipError_t launch_gv4_rounds(const KParams &P, const GSplit &S, uint32_t *hist, 
     const uint64_t grid = (P.n + 4095) / 4096;
     if (grid > 0x7fffffffu) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gv4_hist_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, S, hist);
-    hipLaunchKernelGGL(gv4_scan_kernel, dim3(1), dim3(1024), 0, st, hist, rstart, n_rounds);
+    hipLaunchKernelGGL(gv4_scan_kernel, dim3(1), dim3(1024), 0, st, hist, rstart, n_rounds, desc);
     hipLaunchKernelGGL(gv4_place_kernel, dim3((unsigned)grid), dim3(1024), 0, st, P, S, rstart, cursor, desc);
     return hipGetLastError();
 }

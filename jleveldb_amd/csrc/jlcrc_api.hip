@@ -238,8 +238,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     uint32_t *parts = (uint32_t *)(sp + 256 + a_bb + a_big);
     hipError_t e = hipMemsetAsync(buf, 0, 2 * ab, st);  // hist, cursor
     if (e == hipSuccess) e = hipMemsetAsync(SP.ctl, 0, 16, st);
-    // null groups of partial rounds: idx = kGNull (the kernel mirrors group 0 there)
-    if (e == hipSuccess) e = hipMemsetAsync(desc, 0xff, max_rounds * sizeof(jlk::GDesc) * 8, st);
+    // (empty groups of partial rounds are marked by the scan kernel: no clearing)
     if (e == hipSuccess) e = jlk::launch_gv4_rounds(P, SP, hist, cursor, rstart, desc, n_rounds, st);
     A.parts = parts;
     A.desc = desc;
