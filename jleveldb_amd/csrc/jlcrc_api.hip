@@ -654,22 +654,21 @@ static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, 
     const uint64_t nb = (log_bytes + 32767) / 32768;
     *n_events = 0;
     if (nb == 0) return JL_OK;
-    JL_HIP(c.ws_cnt.ensure(nb * 8));
-    JL_HIP(c.ws_start.ensure(nb * 8));
+    JL_HIP(c.ws_cnt.ensure((nb + 1) * 8));  // cnt[nb] = 0: the exclusive scan's start[nb] is the total
+    JL_HIP(c.ws_start.ensure((nb + 1) * 8));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLogSlots * sizeof(jlk::LogSlot)));
     uint64_t *cnt = (uint64_t *)c.ws_cnt.p, *start = (uint64_t *)c.ws_start.p;
     jlk::LogSlot *slots = (jlk::LogSlot *)c.ws_slot.p;
     JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 0, cnt, nullptr, nullptr, nullptr, nullptr, slots,
                                 st));
+    JL_HIP(hipMemsetAsync(cnt + nb, 0, 8, st));
     size_t tmp = 0;
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, start, (int)nb, st));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, start, (int)(nb + 1), st));
     JL_HIP(c.ws_tmp.ensure(tmp));
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, tmp, cnt, start, (int)nb, st));
-    uint64_t last_start = 0, last_cnt = 0;
-    JL_HIP(hipMemcpyAsync(&last_start, start + nb - 1, 8, hipMemcpyDeviceToHost, st));
-    JL_HIP(hipMemcpyAsync(&last_cnt, cnt + nb - 1, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, tmp, cnt, start, (int)(nb + 1), st));
+    uint64_t total = 0;  // one copy back: the event count sizes the next buffers
+    JL_HIP(hipMemcpyAsync(&total, start + nb, 8, hipMemcpyDeviceToHost, st));
     JL_HIP(hipStreamSynchronize(st));
-    const uint64_t total = last_start + last_cnt;
     *n_events = total;
     if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
     if (total == 0) return JL_OK;

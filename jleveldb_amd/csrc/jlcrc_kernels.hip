@@ -514,7 +514,6 @@ __global__ __launch_bounds__(1024) void crc_general_kernel(const uint4 *__restri
 // verification of the OK events is done by crc_general_kernel afterwards and
 // applied by log_finalize_kernel.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
 
 __device__ __forceinline__ void log_put(LogEvent *ev, uint64_t *d_off, uint32_t *d_len, uint64_t at, uint64_t p,
                                         uint32_t length, uint32_t type, uint8_t kind) {
@@ -554,9 +553,10 @@ __global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, 
             if (eof && rem > 0) { kind = 6; stop = true; }
             else break;
         } else {
-            const uint8_t *h = log + p;
-            length = rd16(h + 4);
-            type = h[6];
+            // header bytes 3..6 in one unaligned dword load: [crc3][len lo][len hi][type]
+            const uint32_t w = *(const u32u *)(log + p + 3);
+            length = (w >> 8) & 0xffffu;
+            type = w >> 24;
             if (7u + (uint64_t)length > rem) { kind = eof ? 5 : 3; stop = true; }
             else if (type == 0 && length == 0) { kind = 4; stop = true; }
             else kind = 1;
