@@ -1,7 +1,7 @@
 // general_v4.hip — general-path engine on the v4 lane layout (variable block
 // lengths and alignment, per-block init/suffix, table/log verify epilogues).
 // Compiled once per mode (-DJL_MODE=k, Makefile); the mode-independent helper
-// kernels (keys, runs, round descriptors) live in the JL_MODE == 0 object.
+// kernels (rounds pipeline, split-block combine) live in the JL_MODE == 0 object.
 //
 // Work unit: a ROUND of up to 8 blocks with the same step count K, processed by
 // one wave exactly as the 4 KiB kernel (fixed_v4.hip) processes 8 blocks: 8
@@ -17,9 +17,11 @@
 // byte of the block never leaves the block's pages, so no load can fault.
 // Pad bytes are masked to zero in the first / last step; zeros in front are
 // free, the d zeros behind advance the state by z^d, which the epilogue undoes
-// with z^-(2^i) for the set bits i of d.  Rounds only hold blocks of one K
-// (the host pipeline sorts blocks by K and cuts every run of equal K into
-// rounds of 8; 128-B aligned fixed-stride batches need no sort).
+// inside shifts it does anyway (d = 16a + 4c + e: chain tables z^-4(j+c), lane
+// column l+a, one z^-e).  Rounds only hold blocks of one K (a counting sort by
+// K, the rounds pipeline at the end of this file, cuts every bin into rounds
+// of 8; 128-B aligned fixed-stride batches need none).  Blocks above 512 KiB
+// (crc mode) run as chunks folded per block afterwards (gv4_combine_kernel).
 //
 // Seeding needs no state shift (as in the stream kernel): W = slice4^-1(~init)
 // is fed as the 4 data bytes just before the block, i.e. at virtual bytes
@@ -33,7 +35,8 @@
 //   K       steps 0..K-1 (0 and K-1 mask their pads)
 // The ring (P = 8 entries, s_waitcnt vmcnt(P-2) before each use, refill right
 // after) runs across rounds, so the HBM stream never drains.  Round
-// descriptors are read with scalar loads (lgkmcnt, never vmcnt).
+// descriptors are prefetched by vector loads into pinned registers (long
+// rounds) or read with scalar loads (lgkmcnt, never the hand-counted vmcnt).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
