@@ -683,7 +683,9 @@ static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, 
         P.len = (const uint32_t *)c.ws_len.p;
         P.out8 = (uint8_t *)c.ws_ok.p;
         if (int r = run_general(P, st)) return r;
-        JL_HIP(jlk::launch_log_finalize(nb, start, cnt, (const uint8_t *)c.ws_ok.p, (jlk::LogEvent *)d_events, 1, st));
+        // firstbad scratch: the walk's slot workspace is free again (n_blocks words fit in it)
+        JL_HIP(jlk::launch_log_finalize(nb, start, cnt, (const uint8_t *)c.ws_ok.p, (jlk::LogEvent *)d_events, 1, total,
+                                        (unsigned long long *)c.ws_slot.p, st));
     }
     JL_HIP(hipStreamSynchronize(st));
     return JL_OK;

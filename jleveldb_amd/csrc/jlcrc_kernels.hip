@@ -784,8 +784,36 @@ hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, ui
     return hipGetLastError();
 }
 
+// Event-parallel form of log_finalize_kernel (r1: one thread per 32 KiB block
+// walked its events serially): the first failing OK event of each block by an
+// atomicMin, then every event of the block compares its index with it.
+__global__ void log_firstbad_kernel(uint64_t n_events, const uint8_t *__restrict__ ok, const LogEvent *__restrict__ ev,
+                                    unsigned long long *__restrict__ firstbad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_events) return;
+    if (ev[i].kind == 1 && !ok[i]) atomicMin(&firstbad[ev[i].offset / 32768u], (unsigned long long)i);
+}
+__global__ void log_apply_kernel(uint64_t n_events, const unsigned long long *__restrict__ firstbad,
+                                 LogEvent *__restrict__ ev) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_events) return;
+    const unsigned long long fb = firstbad[ev[i].offset / 32768u];
+    if (i == fb) ev[i].kind = 2;
+    else if (i > fb) ev[i].kind = 0;
+}
+
 hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
-                               LogEvent *ev, int checksum, hipStream_t st) {
+                               LogEvent *ev, int checksum, uint64_t n_events, unsigned long long *firstbad,
+                               hipStream_t st) {
+    if (firstbad) {  // event-parallel (firstbad: n_blocks words of scratch)
+        if (!checksum || n_events == 0) return hipSuccess;
+        hipError_t e = hipMemsetAsync(firstbad, 0xff, n_blocks * sizeof(unsigned long long), st);
+        if (e != hipSuccess) return e;
+        const unsigned g = (unsigned)((n_events + 255) / 256);
+        hipLaunchKernelGGL(log_firstbad_kernel, dim3(g), dim3(256), 0, st, n_events, ok, ev, firstbad);
+        hipLaunchKernelGGL(log_apply_kernel, dim3(g), dim3(256), 0, st, n_events, firstbad, ev);
+        return hipGetLastError();
+    }
     unsigned grid = (unsigned)((n_blocks + 255) / 256);
     hipLaunchKernelGGL(log_finalize_kernel, dim3(grid), dim3(256), 0, st, n_blocks, starts, counts, ok, ev, checksum);
     return hipGetLastError();

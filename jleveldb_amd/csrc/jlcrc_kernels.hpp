@@ -127,8 +127,12 @@ hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks,
 // incl[i] = sum of weights of blocks 0..i (weight = len + per-block overhead);
 // part[w] = first block of wave w (part[0] = 0, part[parts] = n).
 hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, uint64_t *part, hipStream_t st);
+// applies the CRC results to the events (BAD_CRC at a block's first failure,
+// its later events hidden); firstbad (n_blocks words of scratch) selects the
+// event-parallel form, null the block-serial one
 hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
-                               LogEvent *ev, int checksum, hipStream_t st);
+                               LogEvent *ev, int checksum, uint64_t n_events, unsigned long long *firstbad,
+                               hipStream_t st);
 hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, const uint64_t *frag_hdr_off,
                            const uint32_t *frag_len, uint64_t n_frags, uint8_t *log, uint64_t *pay_off, hipStream_t st);
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st);
