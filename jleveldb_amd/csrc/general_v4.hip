@@ -753,6 +753,8 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uin
         wave_rank(b, h, hist);
         if (b >= kLdsBins && b < kGSoloKey) atomicMax(&hist[kGSoloKey + 1u], b);  // rare: blocks >= 512 KiB
     }
+    __shared__ uint32_t wg_max;
+    if (threadIdx.x == 0) wg_max = 0;
     __syncthreads();
     uint32_t mx = 0;
     for (uint32_t b = threadIdx.x; b < kLdsBins; b += blockDim.x)
@@ -760,7 +762,9 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uin
             atomicAdd(&hist[b], h[b]);
             mx = b;
         }
-    if (mx) atomicMax(&hist[kGSoloKey + 1u], mx);
+    if (mx) atomicMax(&wg_max, mx);  // LDS: one global atomic per workgroup below
+    __syncthreads();
+    if (threadIdx.x == 0 && wg_max) atomicMax(&hist[kGSoloKey + 1u], wg_max);
 }
 
 // hist[kGSoloKey + 1] holds the largest non-solo bin (atomicMax in the hist kernel):
