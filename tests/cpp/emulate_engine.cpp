@@ -155,6 +155,37 @@ static uint32_t emulate_gv4(const std::vector<uint32_t>& img, const uint8_t* blk
     return ~nib(img, kG4EDword + 128 * (d & 3), total);
 }
 
+// The split-block fold (gv4_combine_kernel): chunk raw states from state 0,
+// folded lane-sequentially then by a 6-level tree with z^L from the aux
+// z^(2^k) tables, plus z^n(~init).
+static uint32_t zpow_aux(const std::vector<uint32_t>& aux, uint32_t s, uint32_t L) {
+    for (int k = 0; k < 32; k++)
+        if ((L >> k) & 1u) {
+            uint32_t r = 0;
+            for (int q = 0; q < 8; q++) r ^= aux[kAuxZpow + 128 * k + 16 * q + ((s >> (4 * q)) & 15)];
+            s = r;
+        }
+    return s;
+}
+
+static uint32_t emulate_split(const std::vector<uint32_t>& aux, const uint8_t* blk, uint32_t n, uint32_t cs,
+                              uint32_t init) {
+    const uint32_t m = (n + cs - 1) / cs, L = n - (m - 1) * cs, per = (m + 63) / 64;
+    uint32_t s[64] = {0}, bytes[64] = {0};
+    for (uint32_t t = 0; t < 64; t++)
+        for (uint32_t c = t * per; c < m && c < (t + 1) * per; c++) {
+            const uint32_t len = c + 1 == m ? L : cs;
+            s[t] = zpow_aux(aux, s[t], len) ^ ref_update(0, blk + (size_t)c * cs, len);
+            bytes[t] += len;
+        }
+    for (uint32_t off = 1; off < 64; off <<= 1)
+        for (uint32_t t = 0; t + off < 64; t += 2 * off) {
+            s[t] = zpow_aux(aux, s[t], bytes[t + off]) ^ s[t + off];
+            bytes[t] += bytes[t + off];
+        }
+    return ~(zpow_aux(aux, ~init, n) ^ s[0]);
+}
+
 int main() {
     auto img = build_lds_image();
     std::mt19937_64 rng(42);
@@ -199,6 +230,20 @@ int main() {
                 const uint32_t got = emulate_gv4(imgg, blk, n, f, init, q);
                 cases++;
                 if (want != got && bad++ < 10) printf("gv4 mismatch n=%u f=%u q=%d %08x %08x\n", n, f, q, want, got);
+            }
+    }
+    {
+        auto aux = build_aux();
+        std::vector<uint8_t> big(3 << 20);
+        for (auto& b : big) b = (uint8_t)rng();
+        for (uint32_t n : {1u, 1000u, 65536u, 65537u, 200000u, (uint32_t)big.size() - 7})
+            for (uint32_t cs : {128u, 4096u, 65536u}) {
+                if ((n + cs - 1) / cs > 2048) continue;
+                const uint32_t init = (uint32_t)rng();
+                const uint32_t want = ~ref_update(~init, big.data(), n);
+                const uint32_t got = emulate_split(aux, big.data(), n, cs, init);
+                cases++;
+                if (want != got && bad++ < 10) printf("split mismatch n=%u cs=%u %08x %08x\n", n, cs, want, got);
             }
     }
     printf("%d cases, %d mismatches\n", cases, bad);
