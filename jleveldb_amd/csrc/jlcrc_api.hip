@@ -231,13 +231,15 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     uint32_t *n_rounds = (uint32_t *)(buf + 3 * ab + ad);
     char *sp = buf + 3 * ab + ad + 256;
     jlk::GSplit SP;
-    SP.ctl = (unsigned long long *)sp;
+    // the split counters sit in the padding after hist[nb] (cleared with hist and cursor)
+    static_assert(((((uint64_t)jlk::kGSoloKey + 2) * 4 + 7) & ~7ull) + 16 <= (((uint64_t)jlk::kGSoloKey + 2) * 4 + 255 & ~255ull),
+                  "split counters must fit in hist's padding");
+    SP.ctl = (unsigned long long *)(buf + ((((uint64_t)jlk::kGSoloKey + 2) * 4 + 7) & ~7ull));
     SP.bigbase = (uint32_t *)(sp + 256);
     SP.big = (jlk::GBig *)(sp + 256 + a_bb);
     SP.part_cap = (uint32_t)std::min<uint64_t>(part_cap, 0x7fffffffu);
     uint32_t *parts = (uint32_t *)(sp + 256 + a_bb + a_big);
     hipError_t e = hipMemsetAsync(buf, 0, 2 * ab, st);  // hist, cursor
-    if (e == hipSuccess) e = hipMemsetAsync(SP.ctl, 0, 16, st);
     // (empty groups of partial rounds are marked by the scan kernel: no clearing)
     if (e == hipSuccess) e = jlk::launch_gv4_rounds(P, SP, hist, cursor, rstart, desc, n_rounds, st);
     A.parts = parts;
