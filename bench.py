@@ -131,22 +131,35 @@ def secondary_c3(dev, stream, steps, warmup):
     return res
 
 
-def secondary_c5(dev, stream, steps, warmup):
+def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
     """Config C5: streaming WAL verification over 2^17 x 32 KiB log blocks (4 GiB).
 
     The log is produced on the device by the product's batched LogWriter
-    (jl_log_layout + jl_log_emit_dev) from C1-shaped records (1 056-B payload =
-    12-B batch header + 16-B key + 1 KiB value varints included), then verified
-    with jl_log_verify_dev (header walk + per-record masked-CRC check with
-    LogReader.readPhysicalRecord semantics).  Timed device-resident, and
-    copy-inclusive from pinned host memory through jl_log_verify."""
-    rec = 1056
+    (jl_log_layout + jl_log_emit_dev), then verified with jl_log_verify_dev
+    (header walk + per-record masked-CRC check with
+    LogReader.readPhysicalRecord semantics).  Two payload sets (SURVEY.md
+    §8d C5): C1-shaped records (1 056-B payload = 12-B batch header + 16-B key
+    + 1 KiB value), and a mixed 1 B-100 KiB set whose records fragment into
+    FIRST/MIDDLE/LAST across log blocks.  Timed device-resident, and
+    copy-inclusive from pinned host memory through jl_log_verify; the CPU
+    leg times the oracle's readPhysicalRecord walk (1 thread) on the first
+    1 GiB of the same log."""
     target = (1 << 17) * 32768
-    n_rec = target // (rec + 7)
-    lens = np.full(n_rec, rec, np.uint32)
-    offs = np.arange(n_rec, dtype=np.uint64) * rec
+    if mixed:
+        rng = np.random.default_rng(SEED + 7)
+        lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024) + 1).astype(np.uint32)
+        keep = int(np.searchsorted(np.cumsum(lens.astype(np.uint64) + 7 * (lens.astype(np.uint64) // 32761 + 1)),
+                                   target))
+        lens = lens[:keep]
+        label = "C5 WAL verify, 2^17 x 32 KiB blocks, mixed 1 B-100 KiB records (fragmented), device-resident"
+    else:
+        rec = 1056
+        lens = np.full(target // (rec + 7), rec, np.uint32)
+        label = "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident"
+    offs = np.zeros(lens.size, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
     plan = jl.log_layout(offs, lens)
-    src = torch.empty(n_rec * rec, dtype=torch.uint8, device=dev)
+    src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=dev)
     jl.fill_random_dev(src, SEED + 5)
     log = jl.log_emit_dev(src, plan)
     del src
@@ -158,8 +171,8 @@ def secondary_c5(dev, stream, steps, warmup):
     kinds = ev[: n_ev * 16].view(-1, 16)[:, 13].cpu().numpy()
     ok = int((kinds == jl.LOG_OK).sum())
     wall, ms = timed(fn, steps, warmup, stream)
-    res = {"config": "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident",
-           "log_bytes": nb, "records": int(plan["len"].size), "records_ok": ok,
+    res = {"config": label, "log_bytes": nb, "payload_records": int(lens.size),
+           "physical_records": int(plan["len"].size), "records_ok": ok,
            "GiB_per_s": round(nb / (wall / steps) / GIB, 1),
            "achieved_GBps": round((crc_bytes + 7 * plan["len"].size) / (wall / steps) / 1e9, 1),
            "ms_per_step": round(wall / steps * 1e3, 3)}
@@ -174,6 +187,17 @@ def secondary_c5(dev, stream, steps, warmup):
     el = time.perf_counter() - t0
     res["copy_inclusive_GiB_per_s"] = round(nb / el / GIB, 2)
     res["copy_inclusive_records_ok"] = int((hev["kind"] == jl.LOG_OK).sum())
+    if cpu:
+        from oracle import oracle  # cpu_baseline leg only (test infrastructure)
+
+        sample = hn[: 1 << 30]
+        want = oracle.log_events(sample)
+        t0 = time.perf_counter()
+        oracle.log_events(sample)
+        el = time.perf_counter() - t0
+        res["cpu_baseline"] = {"GiB_per_s": round(sample.size / el / GIB, 3), "cores": 1, "kind": "port",
+                               "sample": "first 1 GiB of the same log, oracle readPhysicalRecord walk + CRC",
+                               "records_ok": int((want["kind"] == jl.LOG_OK).sum())}
     return res
 
 
@@ -316,7 +340,9 @@ def main():
         torch.cuda.empty_cache()
         sec.append(secondary_c3(dev, stream, 5, 2))
         torch.cuda.empty_cache()
-        sec.append(secondary_c5(dev, stream, 5, 2))
+        sec.append(secondary_c5(dev, stream, 5, 2, cpu=not args.no_cpu))
+        torch.cuda.empty_cache()
+        sec.append(secondary_c5(dev, stream, 5, 2, mixed=True, cpu=not args.no_cpu))
         result["secondary"] = sec
     if rank == 0:
         print(json.dumps(result), flush=True)
