@@ -1,0 +1,94 @@
+"""Full-size parity at the BASELINE.json configs the bench reports beside C2.
+
+* C3: 1M blocks, k ~ Zipf(1.1) on 1..64, len = 1024(k-1) + 1 + U[0,1023]
+  (1 B - 64 KiB), packed back-to-back in one ~12 GB arena (unaligned starts):
+  every block vs the multithreaded oracle (`oracle.batch`, restating
+  J/util/Crc32C.java:85-93,119-162 and the mask :61-75), plus a one-byte flip
+  that must change exactly that block's CRC.
+* C5: 2^17 x 32 KiB log blocks (4 GiB) written by the product's batched
+  LogWriter (jl_log_layout + jl_log_emit_dev, J/db/LogWriter.java:88-161) from
+  both payload sets (1 056-B C1-shaped records; mixed 1 B - 100 KiB records that
+  fragment FIRST/MIDDLE/LAST), verified device-resident (jl_log_verify_dev) and
+  compared event-for-event with the oracle's readPhysicalRecord walk
+  (J/db/LogReader.java:297-383), clean and with byte flips in three blocks.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+SEED = 0x4A4C4442
+
+
+def _live(ev):
+    ev = ev[ev["kind"] != 0]
+    return np.stack([ev["offset"], ev["length"].astype(np.uint64), ev["type"].astype(np.uint64),
+                     ev["kind"].astype(np.uint64)])
+
+
+def test_full_size_c3_block_for_block(gpu, jl, oracle):
+    import torch
+
+    rng = np.random.default_rng(SEED)
+    n = 1 << 20
+    ks = np.empty(0, dtype=np.int64)
+    while ks.size < n:
+        k = rng.zipf(1.1, 2 * n)
+        ks = np.concatenate([ks, k[k <= 64]])
+    lens = (1024 * (ks[:n] - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    total = int(lens.sum(dtype=np.uint64))
+    arena = torch.empty(total, dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(arena, SEED + 3)
+    d_off = torch.from_numpy(offs.view(np.int64)).to(gpu)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(gpu)
+    got = jl.crc32c_batch_dev(arena, d_off, d_len).cpu().numpy().view(np.uint32)
+    host = arena.cpu().numpy()
+    want = oracle.batch(host, offs, lens, threads=THREADS)
+    assert np.array_equal(got, want)
+    del host
+    victim = 777_777
+    arena[int(offs[victim]) + int(lens[victim]) - 1] ^= 0x40
+    got2 = jl.crc32c_batch_dev(arena, d_off, d_len).cpu().numpy().view(np.uint32)
+    assert list(np.nonzero(got2 != got)[0]) == [victim]
+
+
+@pytest.mark.parametrize("payloads", ["c1_1056", "mixed_1b_100k"])
+def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
+    import torch
+
+    target = (1 << 17) * 32768
+    if payloads == "c1_1056":
+        lens = np.full(target // 1063, 1056, np.uint32)
+    else:
+        rng = np.random.default_rng(SEED + 7)
+        lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024)).astype(np.uint32)
+    offs = np.zeros(lens.size, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    plan = jl.log_layout(offs, lens)
+    src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(src, SEED + 5)
+    log = jl.log_emit_dev(src, plan)
+    del src
+    nb = int(plan["log_bytes"])
+    assert log.numel() == nb
+
+    def check():
+        ev, n = jl.log_verify_dev(log)
+        got = ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)
+        want = oracle.log_events(log.cpu().numpy())
+        g, w = _live(got), _live(want)
+        assert g.shape == w.shape and np.array_equal(g, w)
+        return want
+
+    w = check()
+    assert w.size == plan["len"].size and bool((w["kind"] == jl.LOG_OK).all())
+    # flips in three log blocks: a flipped payload byte is BAD_CRC and drops the
+    # rest of its 32 KiB block (J/db/LogReader.java:359-367); a flipped header
+    # length is a bad-length report.  Either way the walk must match the oracle.
+    for blk in (5, 70_000, (nb >> 15) - 2):
+        log[blk * 32768 + 20_000] ^= 0x01
+    w = check()
+    assert int(((w["kind"] != 0) & (w["kind"] != jl.LOG_OK)).sum()) >= 3
