@@ -230,6 +230,9 @@ def main():
     ap.add_argument("--settle-ms", type=float, default=200.0,
                     help="untimed launches for this long before the warmup steps (clocks ramp up from idle)")
     ap.add_argument("--blocks", type=int, default=1 << 20, help="4 KiB blocks per GPU (C2: 1M)")
+    ap.add_argument("--strong-total", type=int, default=0,
+                    help="strong scaling: split this many 4 KiB blocks over the ranks (C4: 8388608) instead of "
+                         "--blocks per rank")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
@@ -247,8 +250,11 @@ def main():
     jl.init(local)
     stream = torch.cuda.current_stream()
 
-    n = args.blocks
-    sh = shd.weak_shard(rank, world, n)  # rank r holds blocks [r*n, (r+1)*n) of the C4 set
+    if args.strong_total:  # C4 strong: a fixed set split into contiguous ranges
+        sh = shd.strong_shard(rank, world, args.strong_total)
+    else:  # weak: rank r holds blocks [r*n, (r+1)*n) of the C4 set
+        sh = shd.weak_shard(rank, world, args.blocks)
+    n = sh.n_blocks
     data = torch.empty(n * 4096, dtype=torch.uint8, device=dev)
     jl.fill_random_dev(data, SEED, first_word=sh.first_word)  # generated in place
     out = torch.empty(n, dtype=torch.int32, device=dev)
@@ -281,9 +287,12 @@ def main():
     per_launch = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
     kern_ms = sum(per_launch) / args.steps
     wall = shd.job_wall_time(wall, dev)  # max over ranks (no-op at N=1)
-    value = shd.aggregate_rate(n * 4096, world, wall, args.steps)
+    if args.strong_total:
+        value = args.strong_total * 4096 * args.steps / wall / GIB
+    else:
+        value = shd.aggregate_rate(n * 4096, world, wall, args.steps)
     gather_ms = None
-    if world > 1:  # result all-gather: reported beside, not part of the checksum path
+    if world > 1 and (not args.strong_total or args.strong_total % world == 0):  # result all-gather: reported beside, not part of the checksum path
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -307,11 +316,14 @@ def main():
             "settle_launches": settle,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong_total else "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (device splitmix64, seed 0x4A4C4442; rank r = blocks [r*1M,(r+1)*1M) of the C4 set)",
-            "config": {"workload": "C2: 1M x 4 KiB random blocks per GPU, masked CRC32C, device-resident",
+            "data": "synthetic (device splitmix64, seed 0x4A4C4442; rank r = blocks "
+                    f"[{sh.first_block}, {sh.first_block + n}) of the C4 set)",
+            "config": {"workload": (f"C4 strong: {args.strong_total} x 4 KiB blocks split over {world} GPUs"
+                                    if args.strong_total else "C2: 1M x 4 KiB random blocks per GPU")
+                       + ", masked CRC32C, device-resident",
                        "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
             "result_allgather_ms": None if gather_ms is None else round(gather_ms, 3),
             "roofline": {
