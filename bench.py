@@ -333,8 +333,9 @@ def main():
                 "peak": PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
+                # PMC was collected on 1M-block launches; scale to this launch's blocks
+                "traffic": None if traffic is None else round(traffic * n / (1 << 20)),
+                "traffic_source": traffic_src if n == 1 << 20 else f"{traffic_src} x {n}/1048576 blocks",
                 "kernel_ms": round(kern_ms, 4),
                 "kernel_ms_min": round(min(per_launch), 4),
                 "kernel_ms_median": round(float(np.median(per_launch)), 4),
