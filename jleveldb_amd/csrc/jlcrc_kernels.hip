@@ -544,6 +544,11 @@ __global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, 
     const bool eof = (be - bs) < 32768u;
     uint64_t p = bs, cnt = 0;
     uint64_t o = pass ? starts[b] : 0;
+    // header bytes 3..6 in one unaligned dword load: [crc3][len lo][len hi][type].
+    // The next header's load is issued before this record's slot/event store:
+    // on gfx9 vmcnt counts stores too, so a store issued first would put its
+    // write latency on the walk's serial chain.
+    uint32_t w = (be - p >= 7) ? *(const u32u *)(log + p + 3) : 0u;
     for (;;) {
         const uint64_t rem = be - p;
         uint8_t kind = 0;
@@ -553,28 +558,25 @@ __global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, 
             if (eof && rem > 0) { kind = 6; stop = true; }
             else break;
         } else {
-            // header bytes 3..6 in one unaligned dword load: [crc3][len lo][len hi][type]
-            const uint32_t w = *(const u32u *)(log + p + 3);
             length = (w >> 8) & 0xffffu;
             type = w >> 24;
             if (7u + (uint64_t)length > rem) { kind = eof ? 5 : 3; stop = true; }
             else if (type == 0 && length == 0) { kind = 4; stop = true; }
             else kind = 1;
         }
+        const uint64_t pn = p + 7u + length;
+        if (!stop && be - pn >= 7) w = *(const u32u *)(log + pn + 3);
         if (pass) {
             if (!slots || cnt >= kLogSlots) log_put(ev, d_off, d_len, o + cnt, p, length, type, kind);
         } else if (slots && cnt < kLogSlots) {
-            LogSlot sl;
-            sl.off = (uint16_t)(p - bs);
-            sl.length = (uint16_t)length;
-            sl.type = (uint8_t)type;
-            sl.kind = kind;
-            sl.pad = 0;
-            slots[b * kLogSlots + cnt] = sl;
+            // one 8-byte store of the LogSlot {off, length, type, kind, pad} (little endian)
+            static_assert(sizeof(LogSlot) == 8, "LogSlot packs into one dwordx2");
+            reinterpret_cast<uint64_t *>(slots)[b * kLogSlots + cnt] =
+                (uint64_t)(p - bs) | ((uint64_t)length << 16) | ((uint64_t)type << 32) | ((uint64_t)kind << 40);
         }
         cnt++;
         if (stop) break;
-        p += 7u + length;
+        p = pn;
     }
     if (!pass) counts[b] = cnt;
 }
