@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import jleveldb_amd as jl  # noqa: E402
 from jleveldb_amd import shard as shd  # noqa: E402
+from jleveldb_amd import workloads as wl  # noqa: E402
 
 SEED = 0x4A4C4442
 PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
@@ -106,16 +107,9 @@ def cpu_baseline(data, n_blocks, gpu_out, seconds):
 
 def secondary_c3(dev, stream, steps, warmup):
     """Config C3: 1M blocks, k~Zipf(1.1) on 1..64, len = 1024(k-1)+1+U[0,1023], packed, unaligned."""
-    rng = np.random.default_rng(SEED)
-    n = 1 << 20
-    ks = np.empty(0, dtype=np.int64)
-    while ks.size < n:
-        k = rng.zipf(1.1, 2 * n)
-        ks = np.concatenate([ks, k[k <= 64]])
-    ks = ks[:n]
-    lens = (1024 * (ks - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
-    offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    lens = wl.c3_lengths(1 << 20, SEED)
+    n = lens.size
+    offs = wl.packed_offsets(lens)
     total = int(lens.sum(dtype=np.uint64))
     arena = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     jl.fill_random_dev(arena, SEED + 3)
@@ -144,20 +138,12 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
     copy-inclusive from pinned host memory through jl_log_verify; the CPU
     leg times the oracle's readPhysicalRecord walk (1 thread) on the first
     1 GiB of the same log."""
-    target = (1 << 17) * 32768
+    lens = wl.c5_lengths(mixed, seed=SEED)
     if mixed:
-        rng = np.random.default_rng(SEED + 7)
-        lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024) + 1).astype(np.uint32)
-        keep = int(np.searchsorted(np.cumsum(lens.astype(np.uint64) + 7 * (lens.astype(np.uint64) // 32761 + 1)),
-                                   target))
-        lens = lens[:keep]
         label = "C5 WAL verify, 2^17 x 32 KiB blocks, mixed 1 B-100 KiB records (fragmented), device-resident"
     else:
-        rec = 1056
-        lens = np.full(target // (rec + 7), rec, np.uint32)
         label = "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident"
-    offs = np.zeros(lens.size, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    offs = wl.packed_offsets(lens)
     plan = jl.log_layout(offs, lens)
     src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=dev)
     jl.fill_random_dev(src, SEED + 5)
@@ -222,6 +208,28 @@ def copy_inclusive_c2(data):
             "parity_with_device_resident": bool(np.array_equal(ref, got))}
 
 
+def spawn_ranks(gpus: int) -> None:
+    """`bench.py --gpus N` (N > 1) outside torch.distributed.run: launch N ranks,
+    one process per GPU, through torch.distributed.run as a CHILD process (this
+    process has not touched the GPU: device_count() does not initialise it) and
+    exit with its status.  Refuses to run on fewer than N visible GPUs."""
+    import socket
+    import subprocess
+
+    have = torch.cuda.device_count()
+    if have < gpus:
+        print(f"bench.py: --gpus {gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+        sys.exit(2)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,15 +246,21 @@ def main():
     ap.add_argument("--no-secondary", action="store_true")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the process group's size",
+              file=sys.stderr, flush=True)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
     jl.init(local)
     stream = torch.cuda.current_stream()
 
@@ -292,7 +306,7 @@ def main():
     else:
         value = shd.aggregate_rate(n * 4096, world, wall, args.steps)
     gather_ms = None
-    if world > 1 and (not args.strong_total or args.strong_total % world == 0):  # result all-gather: reported beside, not part of the checksum path
+    if world > 1:  # result all-gather (unequal strong shards padded): reported beside, not part of the checksum path
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -346,7 +360,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(data, n, gpu_out, args.cpu_seconds)
-    if world == 1 and not args.no_secondary:
+    if world == 1 and not args.no_secondary and not args.strong_total:  # secondaries describe the 1M-block C2 box
         sec = [copy_inclusive_c2(data)]
         sec[0]["parity_with_device_resident"] &= bool(np.array_equal(gpu_out, out.cpu().numpy().view(np.uint32)))
         del data

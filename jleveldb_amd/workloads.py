@@ -1,0 +1,54 @@
+"""Synthetic inputs of the BASELINE.json configs, shared by bench.py and the
+tests so that the full-size parity tests check exactly the sets the bench
+reports.
+
+All generators are seeded and deterministic; the bytes themselves come from
+jl_fill_random_dev's splitmix64 stream (device) or its oracle twin (host).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x4A4C4442
+LOG_BLOCK = 32768  # J/db/LogFormat.java:52
+C5_LOG_BYTES = (1 << 17) * LOG_BLOCK  # 2^17 x 32 KiB = 4 GiB
+C1_PAYLOAD = 12 + 1 + 1 + 16 + 2 + 1024  # WriteBatch header + tag + varint + 16-B key + varint + 1 KiB value
+
+
+def c3_lengths(n: int = 1 << 20, seed: int = SEED) -> np.ndarray:
+    """Config C3 block sizes: k ~ Zipf(1.1) on {1..64}, len = 1024(k-1) + 1 + U[0,1023]
+    (1 B - 64 KiB)."""
+    rng = np.random.default_rng(seed)
+    ks = np.empty(0, dtype=np.int64)
+    while ks.size < n:
+        k = rng.zipf(1.1, 2 * n)
+        ks = np.concatenate([ks, k[k <= 64]])
+    ks = ks[:n]
+    return (1024 * (ks - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
+
+
+def packed_offsets(lens: np.ndarray) -> np.ndarray:
+    """Offsets of blocks packed back-to-back (unaligned starts)."""
+    offs = np.zeros(lens.size, np.uint64)
+    if lens.size > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return offs
+
+
+def _frag_bytes(lens: np.ndarray) -> np.ndarray:
+    """Upper bound on the log bytes of each record: payload + one 7-B header per
+    started block-sized fragment."""
+    lens = lens.astype(np.uint64)
+    return lens + 7 * (lens // (LOG_BLOCK - 7) + 1)
+
+
+def c5_lengths(mixed: bool, target: int = C5_LOG_BYTES, seed: int = SEED) -> np.ndarray:
+    """Config C5 payload lengths whose LogWriter framing fills about `target`
+    bytes: either C1-shaped records (1 056-B payloads) or a mixed 1 B - 100 KiB
+    set whose records fragment FIRST/MIDDLE/LAST across 32 KiB blocks."""
+    if not mixed:
+        return np.full(target // (C1_PAYLOAD + 7), C1_PAYLOAD, np.uint32)
+    rng = np.random.default_rng(seed + 7)
+    lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024) + 1).astype(np.uint32)
+    keep = int(np.searchsorted(np.cumsum(_frag_bytes(lens)), target))
+    return lens[:keep]

@@ -5,6 +5,11 @@
   every block vs the multithreaded oracle (`oracle.batch`, restating
   J/util/Crc32C.java:85-93,119-162 and the mask :61-75), plus a one-byte flip
   that must change exactly that block's CRC.
+* C4: the 8M x 4 KiB (32 GiB) set on one GPU as its 8 strong shards, each
+  generated in place from its first splitmix64 word as a rank of bench.py
+  --gpus 8 generates it: the shards' results concatenate to the results of one
+  32 GiB launch and equal the oracle block for block; a one-byte flip changes
+  exactly one CRC.
 * C5: 2^17 x 32 KiB log blocks (4 GiB) written by the product's batched
   LogWriter (jl_log_layout + jl_log_emit_dev, J/db/LogWriter.java:88-161) from
   both payload sets (1 056-B C1-shaped records; mixed 1 B - 100 KiB records that
@@ -14,6 +19,9 @@
 """
 import numpy as np
 import pytest
+
+from jleveldb_amd import shard as shd
+from jleveldb_amd import workloads as wl
 
 pytestmark = pytest.mark.gpu
 
@@ -30,15 +38,9 @@ def _live(ev):
 def test_full_size_c3_block_for_block(gpu, jl, oracle):
     import torch
 
-    rng = np.random.default_rng(SEED)
-    n = 1 << 20
-    ks = np.empty(0, dtype=np.int64)
-    while ks.size < n:
-        k = rng.zipf(1.1, 2 * n)
-        ks = np.concatenate([ks, k[k <= 64]])
-    lens = (1024 * (ks[:n] - 1) + 1 + rng.integers(0, 1024, n)).astype(np.uint32)
-    offs = np.zeros(n, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    lens = wl.c3_lengths(1 << 20, SEED)  # the set bench.py reports
+    n = lens.size
+    offs = wl.packed_offsets(lens)
     total = int(lens.sum(dtype=np.uint64))
     arena = torch.empty(total, dtype=torch.uint8, device=gpu)
     jl.fill_random_dev(arena, SEED + 3)
@@ -59,14 +61,8 @@ def test_full_size_c3_block_for_block(gpu, jl, oracle):
 def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
     import torch
 
-    target = (1 << 17) * 32768
-    if payloads == "c1_1056":
-        lens = np.full(target // 1063, 1056, np.uint32)
-    else:
-        rng = np.random.default_rng(SEED + 7)
-        lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024)).astype(np.uint32)
-    offs = np.zeros(lens.size, np.uint64)
-    offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    lens = wl.c5_lengths(payloads == "mixed_1b_100k", seed=SEED)  # the sets bench.py reports
+    offs = wl.packed_offsets(lens)
     plan = jl.log_layout(offs, lens)
     src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
     jl.fill_random_dev(src, SEED + 5)
@@ -92,3 +88,28 @@ def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
         log[blk * 32768 + 20_000] ^= 0x01
     w = check()
     assert int(((w["kind"] != 0) & (w["kind"] != jl.LOG_OK)).sum()) >= 3
+
+
+def test_full_size_c4_strong_shards(gpu, jl, oracle):
+    import torch
+
+    total, world = 8 << 20, 8
+    data = torch.empty(total * 4096, dtype=torch.uint8, device=gpu)  # 32 GiB
+    jl.fill_random_dev(data, SEED)
+    whole = jl.crc32c_fixed_dev(data, 4096, total)
+    for r in range(world):
+        sh = shd.strong_shard(r, world, total)
+        part = torch.empty(sh.n_blocks * 4096, dtype=torch.uint8, device=gpu)
+        jl.fill_random_dev(part, SEED, first_word=sh.first_word)
+        assert torch.equal(part[:1 << 20], data[sh.first_block * 4096:sh.first_block * 4096 + (1 << 20)])
+        got = jl.crc32c_fixed_dev(part, 4096, sh.n_blocks)
+        assert torch.equal(got, whole[sh.first_block:sh.first_block + sh.n_blocks]), f"shard {r}"
+        del part, got
+    torch.cuda.empty_cache()
+    want = oracle.fixed(data.cpu().numpy(), 4096, total, threads=THREADS)
+    ref = whole.cpu().numpy().view(np.uint32)
+    assert np.array_equal(ref, want)
+    victim = 6_543_210
+    data[victim * 4096 + 1234] ^= 0x08
+    got2 = jl.crc32c_fixed_dev(data, 4096, total).cpu().numpy().view(np.uint32)
+    assert list(np.nonzero(got2 != ref)[0]) == [victim]

@@ -130,7 +130,7 @@ __global__ void fill_rand(uint64_t *d, uint64_t words) {
 }
 
 int main(int argc, char **argv) {
-    size_t bytes = (size_t)4 << 30;
+    size_t bytes = (size_t)(argc > 3 ? atoi(argv[3]) : 4) << 30;  // GiB (argv[3]; default 4)
     uint8_t *d;
     uint32_t *sink;
     CK(hipMalloc(&d, bytes));
@@ -191,7 +191,7 @@ int main(int argc, char **argv) {
     for (size_t v = 0; v < vs.size(); v++) {
         std::sort(t[v].begin(), t[v].end());
         float med = t[v][t[v].size() / 2], mn = t[v][0];
-        printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n", vs[v].name, med,
+        printf("{\"variant\": \"%s\", \"GiB\": %zu, \"median_ms\": %.4f, \"GBps_median\": %.1f, \"GBps_best\": %.1f}\n", vs[v].name, bytes >> 30, med,
                bytes / (med * 1e-3) / 1e9, bytes / (mn * 1e-3) / 1e9);
     }
     return 0;
