@@ -75,12 +75,52 @@ def pmc_traffic():
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    return min(16, os.cpu_count() or 1)
+
+
+def best_host_rate(host: np.ndarray, seconds: float = 3.0) -> dict:
+    """Context line (not the baseline): the product's host scalar path
+    (jl_crc32c_value: x86 SSE4.2 crc32, host_crc.cpp) over 64 MiB pieces of the
+    same bytes on all the threads used for the CPU baseline."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    threads = cpu_threads()
+    piece = 64 << 20
+    pieces = [host[i:i + piece] for i in range(0, host.size - piece + 1, piece)] or [host]
+    L = jl.lib()
+
+    def one(a):
+        return L.jl_crc32c_value(a.ctypes.data, a.size)
+
+    done = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while time.perf_counter() - t0 < seconds:
+            list(ex.map(one, pieces))
+            done += sum(a.size for a in pieces)
+    el = time.perf_counter() - t0
+    return {"value": round(done / el / GIB, 2), "unit": "GiB/s", "cores": threads,
+            "kind": "host sse4.2 crc32 (jl_crc32c_value, the product's scalar host path)"}
+
+
 def cpu_baseline(data, n_blocks, gpu_out, seconds):
     from oracle import oracle  # cpu_baseline leg only (test infrastructure)
 
     sample_blocks = min(n_blocks, 1 << 18)  # 1 GiB
     host = data[: sample_blocks * 4096].cpu().numpy()
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     want = oracle.fixed(host, 4096, sample_blocks, threads=threads)
     parity = bool(np.array_equal(want, gpu_out[:sample_blocks]))
     done = 0
@@ -99,13 +139,16 @@ def cpu_baseline(data, n_blocks, gpu_out, seconds):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": cpu_model(),
         "sample": f"{sample_blocks} x 4 KiB blocks (1 GiB) of the same data, {done} passes in {el:.1f} s; "
                   f"oracle/crc32c_oracle.c slicing-by-8 restatement of Crc32C.update; 1-thread rate {one:.2f} GiB/s",
+        "one_thread_GiB_per_s": round(one, 3),
         "parity_with_gpu": parity,
+        "best_host": best_host_rate(host),
     }
 
 
-def secondary_c3(dev, stream, steps, warmup):
+def secondary_c3(dev, stream, steps, warmup, cpu=True):
     """Config C3: 1M blocks, k~Zipf(1.1) on 1..64, len = 1024(k-1)+1+U[0,1023], packed, unaligned."""
     lens = wl.c3_lengths(1 << 20, SEED)
     n = lens.size
@@ -121,6 +164,22 @@ def secondary_c3(dev, stream, steps, warmup):
     res = {"config": "C3 1M mixed Zipf 1 B-64 KiB blocks, one arena, unaligned", "bytes": total,
            "GiB_per_s": round(total / (ms / steps / 1e3) / GIB, 1),
            "achieved_GBps": round(alg / (ms / steps / 1e3) / 1e9, 1), "ms_per_step": round(ms / steps, 3)}
+    if cpu:  # the oracle on the blocks of the arena's first ~1 GiB, all threads and one
+        from oracle import oracle  # cpu_baseline leg only (test infrastructure)
+
+        k = int(np.searchsorted(offs + lens, 1 << 30))
+        sub = arena[: int(offs[k - 1] + lens[k - 1])].cpu().numpy()
+        want = oracle.batch(sub, offs[:k], lens[:k], threads=cpu_threads())
+        parity = bool(np.array_equal(want, out[:k].cpu().numpy().view(np.uint32)))
+        legs = {}
+        for th in (cpu_threads(), 1):
+            t0 = time.perf_counter()
+            oracle.batch(sub, offs[:k], lens[:k], threads=th)
+            legs[th] = sub.size / (time.perf_counter() - t0) / GIB
+        res["cpu_baseline"] = {"GiB_per_s": round(legs[cpu_threads()], 3), "cores": cpu_threads(),
+                               "one_thread_GiB_per_s": round(legs[1], 3), "kind": "port", "cpu_model": cpu_model(),
+                               "sample": f"the first {k} blocks ({sub.size / GIB:.2f} GiB) of the same arena, "
+                                         "oracle slicing-by-8 batch", "parity_with_gpu": parity}
     del arena
     return res
 
@@ -152,16 +211,24 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
     nb = plan["log_bytes"]
     crc_bytes = int(plan["len"].sum(dtype=np.uint64)) + plan["len"].size  # type byte || payload
     events = torch.empty((nb // 7 + 2) * 16, dtype=torch.uint8, device=dev)
-    fn = lambda: jl.log_verify_dev(log, events=events)  # noqa: E731
+    fn = lambda: jl.log_verify_dev(log, jl.LOG_CHECKSUM, events=events)  # noqa: E731
     ev, n_ev = fn()
     kinds = ev[: n_ev * 16].view(-1, 16)[:, 13].cpu().numpy()
     ok = int((kinds == jl.LOG_OK).sum())
     wall, ms = timed(fn, steps, warmup, stream)
+    alg = crc_bytes + 7 * plan["len"].size
     res = {"config": label, "log_bytes": nb, "payload_records": int(lens.size),
            "physical_records": int(plan["len"].size), "records_ok": ok,
-           "GiB_per_s": round(nb / (wall / steps) / GIB, 1),
-           "achieved_GBps": round((crc_bytes + 7 * plan["len"].size) / (wall / steps) / 1e9, 1),
-           "ms_per_step": round(wall / steps * 1e3, 3)}
+           "path": "fused single pass (log_stream.hip: walk + crc + fold) + event scan / compaction",
+           "GiB_per_s": round(nb / (ms / steps / 1e3) / GIB, 1),
+           "achieved_GBps": round(alg / (ms / steps / 1e3) / 1e9, 1),
+           "ms_per_step": round(ms / steps, 3), "wall_ms_per_step": round(wall / steps * 1e3, 3)}
+    fn2 = lambda: jl.log_verify_dev(log, jl.LOG_CHECKSUM_TWO_PASS, events=events)  # noqa: E731
+    ev2, n2 = fn2()
+    same = n2 == n_ev and torch.equal(ev2[: n2 * 16], ev[: n_ev * 16])
+    _, ms2 = timed(fn2, steps, warmup, stream)
+    res["two_pass"] = {"GiB_per_s": round(nb / (ms2 / steps / 1e3) / GIB, 1), "ms_per_step": round(ms2 / steps, 3),
+                       "events_equal_fused": bool(same)}
     host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
     host.copy_(log)
     del log, events
@@ -173,17 +240,31 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
     el = time.perf_counter() - t0
     res["copy_inclusive_GiB_per_s"] = round(nb / el / GIB, 2)
     res["copy_inclusive_records_ok"] = int((hev["kind"] == jl.LOG_OK).sum())
-    if cpu:
+    if cpu:  # the oracle's readPhysicalRecord walk + crc on the log's first 1 GiB: one thread, and
+        # all threads over block-aligned pieces (readPhysicalRecord decides within a 32 KiB block)
+        from concurrent.futures import ThreadPoolExecutor
+
         from oracle import oracle  # cpu_baseline leg only (test infrastructure)
 
         sample = hn[: 1 << 30]
         want = oracle.log_events(sample)
         t0 = time.perf_counter()
         oracle.log_events(sample)
-        el = time.perf_counter() - t0
-        res["cpu_baseline"] = {"GiB_per_s": round(sample.size / el / GIB, 3), "cores": 1, "kind": "port",
-                               "sample": "first 1 GiB of the same log, oracle readPhysicalRecord walk + CRC",
-                               "records_ok": int((want["kind"] == jl.LOG_OK).sum())}
+        one = sample.size / (time.perf_counter() - t0) / GIB
+        th = cpu_threads()
+        step = -(-sample.size // th // 32768) * 32768
+        pieces = [sample[i:i + step] for i in range(0, sample.size, step)]
+        with ThreadPoolExecutor(th) as ex:
+            t0 = time.perf_counter()
+            parts = list(ex.map(oracle.log_events, pieces))
+            allc = sample.size / (time.perf_counter() - t0) / GIB
+        ok_all = sum(int((p["kind"] == jl.LOG_OK).sum()) for p in parts)
+        res["cpu_baseline"] = {"GiB_per_s": round(allc, 3), "cores": th, "one_thread_GiB_per_s": round(one, 3),
+                               "kind": "port", "cpu_model": cpu_model(),
+                               "sample": "first 1 GiB of the same log, oracle readPhysicalRecord walk + CRC "
+                                         f"({th} threads over 32 KiB-block-aligned pieces, and 1 thread)",
+                               "records_ok": int((want["kind"] == jl.LOG_OK).sum()),
+                               "records_ok_threaded": ok_all}
     return res
 
 
@@ -365,7 +446,7 @@ def main():
         sec[0]["parity_with_device_resident"] &= bool(np.array_equal(gpu_out, out.cpu().numpy().view(np.uint32)))
         del data
         torch.cuda.empty_cache()
-        sec.append(secondary_c3(dev, stream, 5, 2))
+        sec.append(secondary_c3(dev, stream, 5, 2, cpu=not args.no_cpu))
         torch.cuda.empty_cache()
         sec.append(secondary_c5(dev, stream, 5, 2, cpu=not args.no_cpu))
         torch.cuda.empty_cache()

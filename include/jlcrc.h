@@ -64,8 +64,34 @@ int jl_shutdown(void);
 const char *jl_last_error(void);
 /* Number of visible HIP devices (0 when none). */
 int jl_device_count(void);
-/* Engine build/version string, e.g. "jlcrc 0.1 gfx950". */
+/* Engine build/version string, e.g. "jlcrc 0.2 gfx950 (...)". */
 const char *jl_version(void);
+
+/* Engine options (process-wide; no reference counterpart).  The defaults are
+ * the measured best; the options exist so tests and tuning can force each
+ * kernel the engine may pick.  Returns JL_ERR_INVALID for an unknown option or
+ * an out-of-range value; jl_get_option returns the current value.
+ *   JL_OPT_GENERAL_PATH      offset/length batches: JL_PATH_AUTO (general v4
+ *                            rounds pipeline, or the one-launch stream kernel for
+ *                            verify batches under 4096 blocks), JL_PATH_STREAM,
+ *                            JL_PATH_GV4
+ *   JL_OPT_STREAM_DEPTH      stream kernel ring entries: 16 (default), 32, 48
+ *   JL_OPT_STREAM_PARTITION  stream kernel: 1 = byte-balanced wave ranges (default),
+ *                            0 = equal block counts
+ *   JL_OPT_SPLIT_CAP         crc batches: chunks available to split blocks above
+ *                            512 KiB (-1 = min(2^20, 2048 n), the default)
+ * Study builds only (make STUDY=1): JL_OPT_FIXED_KERNEL, JL_OPT_GV4_VARIANT. */
+#define JL_OPT_GENERAL_PATH 1
+#define JL_OPT_STREAM_DEPTH 2
+#define JL_OPT_STREAM_PARTITION 3
+#define JL_OPT_SPLIT_CAP 4
+#define JL_OPT_FIXED_KERNEL 100
+#define JL_OPT_GV4_VARIANT 101
+#define JL_PATH_AUTO 0
+#define JL_PATH_STREAM 1
+#define JL_PATH_GV4 2
+int jl_set_option(int option, int64_t value);
+int64_t jl_get_option(int option);
 
 /* ------------------------------------------ device-resident batch checksums */
 /* n_blocks contiguous blocks of block_bytes each starting at d_data
@@ -164,7 +190,16 @@ typedef struct jl_log_event {
  * verifies every record's masked CRC (crc over type || payload, LogWriter.java:147)
  * and truncates each block after its first failure, exactly as the reference
  * reader clears its buffer.  Writes up to `cap` events to d_events and the total
- * to *n_events (host pointer; this call synchronises on the stream). */
+ * to *n_events (host pointer; this call synchronises on the stream once, at the end).
+ * `checksum` (LogReader's checksum flag, J/db/LogReader.java:356):
+ *   JL_LOG_NO_CHECKSUM  header walk only, every record accepted;
+ *   JL_LOG_CHECKSUM     one fused pass over the bytes (walk + crc, log_stream.hip);
+ *                       blocks of more than 256 records take the two-pass path;
+ *   JL_LOG_CHECKSUM_TWO_PASS  header walk, then a batched crc of the records
+ *                       (same results; kept as the fused path's cross-check). */
+#define JL_LOG_NO_CHECKSUM 0
+#define JL_LOG_CHECKSUM 1
+#define JL_LOG_CHECKSUM_TWO_PASS 2
 int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                       uint64_t *n_events, void *stream);
 /* Host-memory form (log = the on-disk .log / MANIFEST bytes); blocking. */

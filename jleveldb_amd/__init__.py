@@ -18,12 +18,14 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjlcrc.so")
+LIB_PATH = os.environ.get("JLCRC_STUDY_LIB") or os.path.join(_HERE, "libjlcrc.so")  # study builds (tools/)
 
 FLAG_MASK = 1
 
 # jl_log_event kinds (include/jlcrc.h)
 LOG_OK, LOG_BAD_CRC, LOG_BAD_LENGTH, LOG_ZERO_SKIP, LOG_EOF_BAD_LENGTH, LOG_EOF_TRUNC = 1, 2, 3, 4, 5, 6
+# checksum argument of the log entry points (include/jlcrc.h): False/0, True/1 (fused single pass), 2 (two-pass)
+LOG_NO_CHECKSUM, LOG_CHECKSUM, LOG_CHECKSUM_TWO_PASS = 0, 1, 2
 LOG_EVENT_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("type", "u1"), ("kind", "u1"), ("pad", "<u2")])
 LOG_RECORD_DTYPE = np.dtype([("offset", "<u8"), ("arena_off", "<u8"), ("size", "<u8")])
 LOG_REPORT_DTYPE = np.dtype([("bytes", "<u8"), ("reason", "<u4"), ("aux", "<u4")])
@@ -77,6 +79,8 @@ def lib() -> ctypes.CDLL:
         "jl_last_error": (ctypes.c_char_p, []),
         "jl_device_count": (i32, []),
         "jl_version": (ctypes.c_char_p, []),
+        "jl_set_option": (i32, [i32, ctypes.c_int64]),
+        "jl_get_option": (ctypes.c_int64, [i32]),
         "jl_crc32c_fixed_dev": (i32, [vp, u64, u64, u32, vp, vp]),
         "jl_crc32c_batch_dev": (i32, [vp, vp, vp, vp, vp, u64, u32, vp, vp]),
         "jl_crc32c_fixed": (i32, [vp, u64, u64, u32, vp]),
@@ -190,6 +194,22 @@ def init(device: int = 0) -> None:
 
 def shutdown() -> None:
     _check(lib().jl_shutdown(), "jl_shutdown")
+
+
+OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 3, 4
+OPT_FIXED_KERNEL, OPT_GV4_VARIANT = 100, 101  # study builds only
+PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
+
+
+def set_option(option: int, value: int) -> int:
+    """jl_set_option: forces a kernel choice / tuning value; returns the previous value."""
+    prev = int(lib().jl_get_option(option))
+    _check(lib().jl_set_option(option, int(value)), "jl_set_option")
+    return prev
+
+
+def get_option(option: int) -> int:
+    return int(lib().jl_get_option(option))
 
 
 def version() -> str:

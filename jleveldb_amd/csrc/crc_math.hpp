@@ -212,6 +212,60 @@ inline std::vector<uint32_t> build_lds_image_gv4() {
     return img;
 }
 
+// Log-stream image (log_stream.hip): region A = the general v4 gap tables
+// (z^(124+t)∘T0, chains 128 B apart); region B re-cut for the fused log kernel
+// (its fold is general_v4.hip's epilogue, with 16 lane-table columns):
+//   [32768, 34816)  lane tables, column b: z^-(16 b) as 8 nibble tables,
+//                   dword 32768 + (p*16 + v)*16 + b       (ls_realign())
+//   [34816, 35712)  U_k = z^-(4k), k = 0..6, nibble tables (chain j: z^-(4 (j + c)))
+//   [35712, 36224)  E_e = z^-e, e = 0..3, nibble tables
+//   kLSMaskDword    39 entries x 4 dwords, entry t + 22 for t in [-22, 16]:
+//                   the byte masks of one data dword when a record header
+//                   starts at byte t of that dword (t may lie before or past it):
+//                     [0] om = bytes < t          (the record that ends at t)
+//                     [1] nm = bytes >= t + 6     (the next record's type byte, payload)
+//                     [2] sd = W0 = slice4^-1(0xffffffff) at bytes [t + 2, t + 6)
+//                          (the next record's crc init, fed as the 4 bytes before it)
+//   kLSStageDword   per-wave header staging, 12 waves x 8 groups x 144 B: the
+//                   group's window and the first 16 B of the next one
+constexpr size_t kLSLaneDword = 32768;
+constexpr size_t kLSShiftDword = 34816;
+constexpr size_t kLSEDword = 35712;
+constexpr size_t kLSMaskDword = 36224;
+constexpr int kLSMaskLo = -22, kLSMaskHi = 16;
+constexpr size_t kLSStageDword = 36384;  // 16-B aligned; 12 x 1152 B: ends at 39840 <= kImageDwords
+inline std::vector<uint32_t> build_lds_image_logstream() {
+    const Tables &T = tables();
+    std::vector<uint32_t> img = build_lds_image_v4(8);  // region A: gap tables for 128-B steps
+    for (size_t i = 32768; i < kImageDwords; i++) img[i] = 0;
+    for (int b = 0; b < 16; b++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kLSLaneDword + (size_t)(p * 16 + v) * 16 + b] = T.zinvn((uint32_t)v << (4 * p), 16u * (uint32_t)b);
+    for (int k = 0; k < 7; k++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kLSShiftDword + (size_t)k * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 4u * (uint32_t)k);
+    for (int e = 0; e < 4; e++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kLSEDword + (size_t)e * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), (uint32_t)e);
+    const uint32_t w0 = slice4_inv(0xffffffffu);
+    for (int t = kLSMaskLo; t <= kLSMaskHi; t++) {
+        uint32_t om = 0, nm = 0, sd = 0;
+        for (int i = 0; i < 4; i++) {
+            if (i < t) om |= 0xffu << (8 * i);
+            if (i >= t + 6) nm |= 0xffu << (8 * i);
+            if (i >= t + 2 && i < t + 6) sd |= ((w0 >> (8 * (i - t - 2))) & 0xffu) << (8 * i);
+        }
+        const size_t e = kLSMaskDword + 4 * (size_t)(t - kLSMaskLo);
+        img[e] = om;
+        img[e + 1] = nm;
+        img[e + 2] = sd;
+    }
+    return img;
+}
+
 // Small global-memory table used by the kernels' scalar epilogues:
 //   [0,256)     T0
 //   [256,512)   inv_top (as u32)

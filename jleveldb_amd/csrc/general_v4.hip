@@ -40,10 +40,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <stdlib.h>
-
 #include "engine_device.hpp"
 
+#ifndef JL_STUDY
+#define JL_STUDY 0
+#endif
 #ifndef JL_MODE
 #error "compile with -DJL_MODE=<jlk::MODE_*>"
 #endif
@@ -581,23 +582,30 @@ namespace jlk {
 
 template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
-    if (getenv("JL_GV4_STRICT"))  // debugging: vmcnt(0) before every ring use
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
-                           zero);
-    else if (A.P.dbg)  // JL_GV4_DEBUG: address range checks
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 4>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
-                           zero);
-    else if (A.no_fast)  // study: per-entry path only
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 5>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
-                           zero);
-    else if (getenv("JL_GV4_FULLTURN"))  // study: whole 8-entry fast turns only
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
-                           zero);
-    else if (getenv("JL_GV4_NONT"))  // study: ring loads without the nt cache policy
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A,
-                           zero);
-    else
-        hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A, zero);
+#if JL_STUDY
+    // study variants: 1 = vmcnt(0) before every ring use, 4 = address checks,
+    // 5 = per-entry path only, 3 = whole 8-entry fast turns, 2 = no nt policy
+    if (A.study) {
+        const int v = A.study;
+        if (v == 1)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 4)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 4>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 5)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 5>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 3)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A, zero);
     return hipGetLastError();
 }
 

@@ -14,8 +14,16 @@
 #include "crc_math.hpp"
 #include "jlcrc_kernels.hpp"
 
+#ifndef JL_STUDY
+#define JL_STUDY 0
+#endif
+
 static_assert(jlmath::kImageBytes == jlk::kImageBytes, "LDS image size mismatch");
 static_assert(sizeof(jl_log_event) == sizeof(jlk::LogEvent), "event layout mismatch");
+static_assert(jlmath::kLSMaskDword * 4 == jlk::kLSMaskByte && jlmath::kLSStageDword * 4 == jlk::kLSStageByte &&
+                  jlmath::kLSLaneDword * 4 == jlk::kLSLaneByte && jlmath::kLSShiftDword * 4 == jlk::kLSShiftByte &&
+                  jlmath::kLSEDword * 4 == jlk::kLSEByte,
+              "log-stream image layout mismatch");
 static_assert(jlmath::kV4SlotDword == jlk::kV4SlotDword && jlmath::kV4UDword * 4 == jlk::kV4U4Byte, "v4 image layout mismatch");
 
 namespace {
@@ -63,11 +71,13 @@ struct Context {
     hipStream_t stream = nullptr;
     void *d_img = nullptr;   // 160 KiB LDS image
     void *d_img_v4[4] = {nullptr, nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block; [3] gv4
+    void *d_img_log = nullptr;  // fused log-verify image (log_stream.hip)
     uint32_t *d_aux = nullptr;
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
     // staging workspace (host-memory APIs, log verify)
     DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp, ws_slot;
+    DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
     // streaming pipeline (jl_crc32c_fixed): two slots, each a device chunk + result
     // buffer, a pinned staging buffer (pageable sources) and its own stream
     struct Slot {
@@ -82,6 +92,22 @@ struct Context {
 Context &ctx() {
     static Context c;
     return c;
+}
+
+// Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
+// batch takes and its tuning.  Defaults are the measured best; tests force the
+// alternatives.  The study options exist in the study build only (make STUDY=1).
+struct Options {
+    int general_path = JL_PATH_AUTO;  // JL_OPT_GENERAL_PATH
+    int stream_depth = 16;            // JL_OPT_STREAM_DEPTH: 16 / 32 / 48 ring entries
+    int partition = 1;                // JL_OPT_STREAM_PARTITION: byte-balanced wave ranges
+    int64_t split_cap = -1;           // JL_OPT_SPLIT_CAP: chunks of split blocks (-1: min(2^20, 2048 n))
+    int fixed_kernel = 7;             // study: JL_OPT_FIXED_KERNEL (7 = the v4 product kernel)
+    int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
+};
+Options &opt() {
+    static Options o;
+    return o;
 }
 
 int ensure_ready() {
@@ -113,6 +139,10 @@ jlk::KParams base_params(const void *d_base, uint64_t n, int mode) {
     return P;
 }
 
+struct U32ToU64 {
+    __host__ __device__ uint64_t operator()(uint32_t v) const { return v; }
+};
+
 // weight of a block for the byte-balanced partition: its bytes plus the
 // per-block fixed cost of the stream kernel (seed, re-alignment, result),
 // roughly that of reading 256 B
@@ -127,7 +157,7 @@ struct BlockWeight {
 // batch is too small to be worth a scan or the blocks have a fixed stride.
 static uint64_t *make_partition(const jlk::KParams &P, uint64_t waves, hipStream_t st, int *rc) {
     *rc = JL_OK;
-    if (!P.off || P.n < 16 * waves || getenv("JL_NO_PARTITION")) return nullptr;
+    if (!P.off || P.n < 16 * waves || !opt().partition) return nullptr;
     hipcub::TransformInputIterator<uint64_t, BlockWeight, const uint32_t *> it(P.len, BlockWeight{P.len_add});
     size_t tmp = 0;
     if (hipcub::DeviceScan::InclusiveSum(nullptr, tmp, it, (uint64_t *)nullptr, (int)P.n, st) != hipSuccess) {
@@ -150,6 +180,7 @@ static uint64_t *make_partition(const jlk::KParams &P, uint64_t waves, hipStream
         *rc = fail(JL_ERR_HIP, "partition failed");
         return nullptr;
     }
+#if JL_STUDY
     if (getenv("JL_PARTITION_DUMP")) {  // debugging: range sizes of the partition
         std::vector<uint64_t> h(waves + 1), hi(P.n);
         (void)hipMemcpyAsync(h.data(), part, (waves + 1) * 8, hipMemcpyDeviceToHost, st);
@@ -160,11 +191,10 @@ static uint64_t *make_partition(const jlk::KParams &P, uint64_t waves, hipStream
             if (h[w + 1] < h[w]) bad++;
             else { mx = std::max(mx, h[w + 1] - h[w]); mn = std::min(mn, h[w + 1] - h[w]); }
         }
-        fprintf(stderr, "partition n=%llu waves=%llu total=%llu incl[0]=%llu part[1]=%llu part[W-1]=%llu min=%llu max=%llu bad=%llu\n",
-                (unsigned long long)P.n, (unsigned long long)waves, (unsigned long long)hi[P.n - 1],
-                (unsigned long long)hi[0], (unsigned long long)h[1], (unsigned long long)h[waves - 1],
-                (unsigned long long)mn, (unsigned long long)mx, (unsigned long long)bad);
+        fprintf(stderr, "partition n=%llu waves=%llu min=%llu max=%llu bad=%llu\n", (unsigned long long)P.n,
+                (unsigned long long)waves, (unsigned long long)mn, (unsigned long long)mx, (unsigned long long)bad);
     }
+#endif
     return part;  // == buf + incl_bytes; freed through free_partition
 }
 
@@ -198,7 +228,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     memset(&A, 0, sizeof(A));
     A.P = P;
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
-    A.no_fast = getenv("JL_GV4_NOFAST") ? 1u : 0u;
+    A.study = (uint32_t)opt().gv4_variant;
     // blocks above kGSplitMin (MODE_CRC) are split into chunks folded afterwards
     const bool can_split = P.mode == jlk::MODE_CRC;
     if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0 &&
@@ -212,10 +242,10 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     // rounds: ceil(c/8) per bin of c blocks <= n/8 + one partial round per bin (2^17 bins),
     // plus one round per solo block (>= 16 MiB each: at most 18432 in 288 GiB)
     const uint64_t nb = (uint64_t)jlk::kGSoloKey + 1;
-    // split blocks: up to part_cap chunks (JL_GV4_PARTCAP: tests), blocks beyond it stay whole
+    // split blocks: up to part_cap chunks (JL_OPT_SPLIT_CAP), blocks beyond it stay whole
     const uint64_t part_cap =
-        can_split ? (getenv("JL_GV4_PARTCAP") ? strtoull(getenv("JL_GV4_PARTCAP"), nullptr, 10)
-                                              : std::min<uint64_t>(1ull << 20, 2048 * n))  // <= 2048 chunks a block
+        can_split ? (opt().split_cap >= 0 ? (uint64_t)opt().split_cap
+                                          : std::min<uint64_t>(1ull << 20, 2048 * n))  // <= 2048 chunks a block
                   : 0;
     const uint64_t vn = n + part_cap;  // blocks and chunks
     const uint64_t max_rounds = vn / 8 + std::min<uint64_t>(vn, nb) + std::min<uint64_t>(n, 18432) + 1;
@@ -245,6 +275,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     A.parts = parts;
     A.desc = desc;
     A.n_rounds = n_rounds;
+#if JL_STUDY
     unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
     if (const char *dbg = getenv("JL_GV4_DEBUG")) {  // "lo:hi" valid load range (hex), debugging only
         A.P.dbg_lo = strtoull(dbg, nullptr, 16);
@@ -253,9 +284,12 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
         if (e == hipSuccess) e = hipMalloc((void **)&d_dbg, sizeof(h_dbg));
         if (e == hipSuccess) e = hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st);
         A.P.dbg = d_dbg;
+        A.study = 4;
     }
+#endif
     if (e == hipSuccess) e = gv4_launch(A, st);
     if (e == hipSuccess && SP.part_cap) e = jlk::launch_gv4_combine(P, SP, parts, st);
+#if JL_STUDY
     if (d_dbg) {
         uint32_t hr = 0;
         if (e == hipSuccess) e = hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st);
@@ -267,6 +301,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
             fprintf(stderr, "  round %llu entry %llu lane %llu addr/idx %llx\n", h_dbg[1 + 4 * i], h_dbg[2 + 4 * i],
                     h_dbg[3 + 4 * i], h_dbg[4 + 4 * i]);
     }
+#endif
     (void)hipFreeAsync(buf, st);
     JL_HIP(e);
     return JL_OK;
@@ -274,21 +309,18 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
 
 int run_general(const jlk::KParams &P, hipStream_t st) {
     if (P.n == 0) return JL_OK;
-    // A/B knobs (tuning only; defaults are the measured best): JL_GENERAL=chunk
-    // selects the r1 chunked kernel, JL_STREAM_DEPTH the stream kernel's ring
-    // depth (16/32/48), JL_NO_PARTITION the count split instead of bytes
-    const char *e_g = getenv("JL_GENERAL");
-    const int depth = getenv("JL_STREAM_DEPTH") ? atoi(getenv("JL_STREAM_DEPTH")) : 16;
     // general v4 (general_v4.hip) is the default for the crc / table-verify /
     // log-verify modes (r1 A/B: C3 2.38 vs 2.64 ms, C5 0.81 vs 0.93 ms, C2 through
-    // offsets 0.95 vs 1.04 ms), except for small sorted batches, where its ~12
-    // pipeline launches cost more than the stream kernel's one;
-    // JL_GENERAL=stream / gv4 force either
-    // (crc batches always take gv4: a few huge blocks there are split across waves)
+    // offsets 0.95 vs 1.04 ms), except for small sorted verify batches, where its
+    // ~12 pipeline launches cost more than the stream kernel's one; crc batches
+    // always take gv4, which splits a few huge blocks across waves.
+    // JL_OPT_GENERAL_PATH forces either.
+    const Options &o = opt();
     const bool small = P.off && P.n < 4096 && P.mode != jlk::MODE_CRC;
-    const bool want_gv4 = e_g ? !strcmp(e_g, "gv4") : !small;
+    const bool want_gv4 = o.general_path == JL_PATH_GV4 || (o.general_path == JL_PATH_AUTO && !small);
     if (want_gv4 && gv4_eligible(P)) return run_gv4(P, st);
-    if (e_g && !strcmp(e_g, "chunk") && !getenv("JL_STREAM_DEBUG")) {
+#if JL_STUDY
+    if (o.general_path == 3 && !getenv("JL_STREAM_DEBUG")) {  // the r1 chunked kernel
         JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
         return JL_OK;
     }
@@ -301,21 +333,19 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
         JL_HIP(hipMalloc((void **)&d_dbg, sizeof(h_dbg)));
         JL_HIP(hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st));
         Q.dbg = d_dbg;
-        JL_HIP(jlk::launch_stream(ctx().d_img, Q, nullptr, grid_for(P.n), depth, st));
+        JL_HIP(jlk::launch_stream(ctx().d_img, Q, nullptr, grid_for(P.n), o.stream_depth, st));
         JL_HIP(hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st));
         JL_HIP(hipStreamSynchronize(st));
         (void)hipFree(d_dbg);
         fprintf(stderr, "JL_STREAM_DEBUG mode=%d n=%llu bad=%llu\n", P.mode, (unsigned long long)P.n, h_dbg[0]);
-        for (unsigned long long i = 0; i < h_dbg[0] % 1000000ull && i < 256; i++)
-            fprintf(stderr, "  block %llu entry %llu lane %llu addr %llx (base %llx)\n", h_dbg[1 + 4 * i], h_dbg[2 + 4 * i],
-                    h_dbg[3 + 4 * i], h_dbg[4 + 4 * i], (unsigned long long)(uintptr_t)P.base);
         return JL_OK;
     }
+#endif
     const int grid = grid_for(P.n);
     int rc = JL_OK;
     uint64_t *part = make_partition(P, (uint64_t)grid * 16, st, &rc);
     if (rc) return rc;
-    const hipError_t e = jlk::launch_stream(ctx().d_img, P, part, grid, depth, st);
+    const hipError_t e = jlk::launch_stream(ctx().d_img, P, part, grid, o.stream_depth, st);
     free_partition(P, part, st);
     JL_HIP(e);
     return JL_OK;
@@ -330,7 +360,60 @@ extern "C" {
 
 const char *jl_last_error(void) { return g_err.c_str(); }
 
-const char *jl_version(void) { return "jlcrc 0.1 gfx950 (lane-interleaved slicing-by-4, LDS gap tables)"; }
+const char *jl_version(void) {
+    return "jlcrc 0.2 gfx950 (v4: 8 lanes per block, 128-B steps, 4 chains per lane through LDS gap tables"
+#if JL_STUDY
+           "; study build"
+#endif
+           ")";
+}
+
+int jl_set_option(int option, int64_t value) {
+    Options &o = opt();
+    switch (option) {
+    case JL_OPT_GENERAL_PATH:
+        if (value < JL_PATH_AUTO || value > (JL_STUDY ? 3 : JL_PATH_GV4)) break;
+        o.general_path = (int)value;
+        return JL_OK;
+    case JL_OPT_STREAM_DEPTH:
+        if (value != 16 && value != 32 && value != 48) break;
+        o.stream_depth = (int)value;
+        return JL_OK;
+    case JL_OPT_STREAM_PARTITION:
+        if (value != 0 && value != 1) break;
+        o.partition = (int)value;
+        return JL_OK;
+    case JL_OPT_SPLIT_CAP:
+        if (value < -1 || value > 0x7fffffff) break;
+        o.split_cap = value;
+        return JL_OK;
+#if JL_STUDY
+    case JL_OPT_FIXED_KERNEL:
+        o.fixed_kernel = (int)value;
+        return JL_OK;
+    case JL_OPT_GV4_VARIANT:
+        if (value < 0 || value > 5) break;
+        o.gv4_variant = (int)value;
+        return JL_OK;
+#endif
+    default:
+        return fail(JL_ERR_INVALID, "jl_set_option: unknown option " + std::to_string(option));
+    }
+    return fail(JL_ERR_INVALID, "jl_set_option: value out of range for option " + std::to_string(option));
+}
+
+int64_t jl_get_option(int option) {
+    const Options &o = opt();
+    switch (option) {
+    case JL_OPT_GENERAL_PATH: return o.general_path;
+    case JL_OPT_STREAM_DEPTH: return o.stream_depth;
+    case JL_OPT_STREAM_PARTITION: return o.partition;
+    case JL_OPT_SPLIT_CAP: return o.split_cap;
+    case JL_OPT_FIXED_KERNEL: return o.fixed_kernel;
+    case JL_OPT_GV4_VARIANT: return o.gv4_variant;
+    default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
+    }
+}
 
 int jl_device_count(void) {
     int n = 0;
@@ -375,6 +458,11 @@ int jl_init(int device) {
         JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
         JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     }
+    {
+        std::vector<uint32_t> li = jlmath::build_lds_image_logstream();
+        JL_HIP(hipMalloc(&c.d_img_log, jlmath::kImageBytes));
+        JL_HIP(hipMemcpy(c.d_img_log, li.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
+    }
     JL_HIP(hipMemcpy(c.d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice));
     JL_HIP(hipMemset(c.d_zero, 0, 4096));
     c.device = device;
@@ -389,7 +477,7 @@ int jl_shutdown(void) {
     (void)hipSetDevice(c.device);
     (void)hipStreamSynchronize(c.stream);
     for (DevBuf *b : {&c.ws_data, &c.ws_off, &c.ws_len, &c.ws_init, &c.ws_sfx, &c.ws_out, &c.ws_cnt, &c.ws_start,
-                      &c.ws_ev, &c.ws_ok, &c.ws_tmp, &c.ws_slot})
+                      &c.ws_ev, &c.ws_ok, &c.ws_tmp, &c.ws_slot, &c.ws_ls, &c.ws_lsev})
         b->release();
     for (auto &sl : c.slot) {
         sl.d_in.release();
@@ -400,6 +488,8 @@ int jl_shutdown(void) {
         sl = Context::Slot();
     }
     (void)hipFree(c.d_img);
+    (void)hipFree(c.d_img_log);
+    c.d_img_log = nullptr;
     for (void *&p : c.d_img_v4) {
         (void)hipFree(p);
         p = nullptr;
@@ -426,25 +516,27 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
     if (!d_data || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: null pointer");
     if (block_bytes > 0xffffffffull) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: block_bytes >= 4 GiB");
     hipStream_t st = pick(stream);
-    if (block_bytes == 4096) {
-        // tuning knobs (A/B only; defaults are the measured best): JL_FIXED_NT, JL_FIXED_DEPTH
-        const char *e_nt = getenv("JL_FIXED_NT"), *e_d = getenv("JL_FIXED_DEPTH"), *e_c = getenv("JL_FIXED_CHAINS");
-        const int nt = e_nt ? atoi(e_nt) : 1;
-        const int depth = e_d ? atoi(e_d) : 2;
-        const int chains = e_c ? atoi(e_c) : 7;  // 7 = v4 (fixed_v4.hip), measured best
-        // v4 path: 7 = 8 lanes/block, 8-slot ring, 1024 threads (default: r1 sustained A/B 0.638 vs
-        // 0.643 ms for the 16-slot ring); 8 = 16 lanes/block; 10 = 16-slot ring without nt;
-        // 11, 12 = (8 slots, 512 threads), (16 slots, 512 threads); 13 = the 16-slot ring
-        if ((chains == 7 || chains == 8 || (chains >= 10 && chains <= 13)) && ((uintptr_t)d_data & 15) == 0) {
+    if (block_bytes == 4096 && ((uintptr_t)d_data & 15) == 0) {
+        const int chains = opt().fixed_kernel;
+        if (chains == 7) {  // the v4 product kernel (fixed_v4.hip): 8 lanes/block, 8-slot ring, 1024 threads
+            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[1], (const uint8_t *)d_data, n_blocks, flags, d_out,
+                                          grid_for(n_blocks), 8, 1, 3, st));
+            return JL_OK;
+        }
+#if JL_STUDY
+        // study kernels: 8 = v4 16 lanes/block; 10 = v4 16-slot ring without nt; 11, 12 = v4 (8 slots, 512
+        // threads), (16 slots, 512 threads); 13 = v4 16-slot ring; 2..6, 101..104 = the r1 kernels
+        if (chains == 8 || (chains >= 10 && chains <= 13)) {
             const int lpb = chains == 8 ? 16 : 8;
-            const int shape = chains == 7 ? 3 : (chains == 11 || chains == 12) ? chains - 10 : 0;
-            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[lpb == 4 ? 0 : lpb == 8 ? 1 : 2], (const uint8_t *)d_data,
-                                          n_blocks, flags, d_out, grid_for(n_blocks), lpb, chains != 10, shape, st));
+            const int shape = (chains == 11 || chains == 12) ? chains - 10 : 0;
+            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[lpb == 8 ? 1 : 2], (const uint8_t *)d_data, n_blocks, flags,
+                                          d_out, grid_for(n_blocks), lpb, chains != 10, shape, st));
             return JL_OK;
         }
         JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
-                                   ctx().d_scratch, grid_for(n_blocks), nt, depth, chains, st));
+                                   ctx().d_scratch, grid_for(n_blocks), 1, 1, chains, st));
         return JL_OK;
+#endif
     }
     jlk::KParams P = base_params(d_data, n_blocks, jlk::MODE_CRC);
     P.fixed_bytes = block_bytes;
@@ -650,9 +742,71 @@ int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uin
     return JL_OK;
 }
 
+// Fused path (log_stream.hip): one streaming kernel walks and verifies every
+// block, a scan of the per-block event counts places them, one compaction
+// kernel writes them in file order; one synchronisation at the end.  Blocks
+// with more than kLogStreamCap events (average record < 121 B) do not fit the
+// per-block slots: *fallback is set and nothing is written.
+constexpr uint32_t kLogStreamCap = 256;
+
+static int log_verify_stream(const void *d_log, uint64_t log_bytes, jl_log_event *d_events, uint64_t cap,
+                             uint64_t *n_events, hipStream_t st, bool *fallback) {
+    Context &c = ctx();
+    *fallback = false;
+    const uint64_t nb = (log_bytes + 32767) / 32768;
+    if (nb >= (1ull << 31)) {
+        *fallback = true;
+        return JL_OK;
+    }
+    // ws_ls: count[nb + 1] | first_bad[nb] | overflow | starts[nb + 1] (u64, 8-B aligned)
+    const size_t cnt_b = (nb + 1) * 4, fb_b = nb * 4, flag_b = 4;
+    const size_t st_off = (cnt_b + fb_b + flag_b + 7) & ~(size_t)7;
+    JL_HIP(c.ws_ls.ensure(st_off + (nb + 1) * 8));
+    JL_HIP(c.ws_lsev.ensure(nb * kLogStreamCap * sizeof(jlk::LogEvent)));
+    char *ws = (char *)c.ws_ls.p;
+    jlk::LogStreamArgs A;
+    A.log = (const uint8_t *)d_log;
+    A.size = log_bytes;
+    A.n_blocks = (uint32_t)nb;
+    A.cap = kLogStreamCap;
+    A.slots = (jlk::LogEvent *)c.ws_lsev.p;
+    A.count = (uint32_t *)ws;
+    A.first_bad = (uint32_t *)(ws + cnt_b);
+    A.overflow = (uint32_t *)(ws + cnt_b + fb_b);
+    uint64_t *start = (uint64_t *)(ws + st_off);
+    JL_HIP(hipMemsetAsync(A.count + nb, 0, 4, st));  // count[nb] = 0: start[nb] is the total
+    JL_HIP(hipMemsetAsync(A.overflow, 0, 4, st));
+    JL_HIP(jlk::launch_logstream(c.d_img_log, A, c.cus, st));
+    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
+    size_t tmp = 0;
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, start, (int)(nb + 1), st));
+    JL_HIP(c.ws_tmp.ensure(tmp));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, tmp, it, start, (int)(nb + 1), st));
+    JL_HIP(jlk::launch_logstream_compact(A, start, (jlk::LogEvent *)d_events, cap, st));
+    uint64_t total = 0;
+    uint32_t over = 0;
+    JL_HIP(hipMemcpyAsync(&total, start + nb, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipMemcpyAsync(&over, A.overflow, 4, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipStreamSynchronize(st));
+    if (over) {
+        *fallback = true;
+        return JL_OK;
+    }
+    *n_events = total;
+    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    return JL_OK;
+}
+
 static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                            uint64_t *n_events, hipStream_t st) {
     Context &c = ctx();
+    if (checksum == 1) {  // JL_LOG_CHECKSUM: the fused single-pass path, unless a block overflows its slots
+        bool fallback = false;
+        *n_events = 0;
+        if (log_bytes == 0) return JL_OK;
+        if (int r = log_verify_stream(d_log, log_bytes, d_events, cap, n_events, st, &fallback)) return r;
+        if (!fallback) return JL_OK;
+    }
     const uint64_t nb = (log_bytes + 32767) / 32768;
     *n_events = 0;
     if (nb == 0) return JL_OK;

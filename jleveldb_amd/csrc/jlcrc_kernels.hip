@@ -1,6 +1,9 @@
-// jlcrc_kernels.hip — CDNA4 (gfx950) kernels of the masked-CRC32C engine.
+// jlcrc_kernels.hip — CDNA4 (gfx950) kernels of the masked-CRC32C engine:
+// the log walk / finalize / copy kernels, the partition, fill and read-stream
+// helpers, and — in the study build only (make STUDY=1, -DJL_STUDY=1) — the
+// round-1 kernels the v4 and general-v4 paths superseded, kept for A/B:
 //
-// One wave (64 lanes) owns one block at a time.  A block of n bytes is viewed
+// [study] One wave (64 lanes) owns one block at a time.  A block of n bytes is viewed
 // end-aligned as K = ceil(n/256) "steps" of 256 bytes (f = 256K - n virtual
 // zero bytes in front); in step k lane l owns the 4-byte word at virtual offset
 // 256k + 4l.  Every step is one coalesced 256-B wave load (global_load_dword)
@@ -20,8 +23,13 @@
 
 #include "engine_device.hpp"
 
+#ifndef JL_STUDY
+#define JL_STUDY 0
+#endif
+
 namespace jlk {
 
+#if JL_STUDY
 // ---------------------------------------------------------------------------
 // Fast path: n_blocks contiguous 4 KiB blocks (one 16-step chunk each, f = 0).
 // Ping-pong register buffers: the 16 loads of the wave's next block are issued
@@ -507,6 +515,8 @@ __global__ __launch_bounds__(1024) void crc_general_kernel(const uint4 *__restri
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#endif  // JL_STUDY
+
 // ---------------------------------------------------------------------------
 // Log walk (LogReader.readPhysicalRecord header decisions per 32 KiB block,
 // J/db/LogReader.java:297-383).  One thread per block; pass 0 counts events,
@@ -702,6 +712,7 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t *__restr
 // ----------------------------------------------------------------- launchers
 namespace jlk {
 
+#if JL_STUDY
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st) {
@@ -757,6 +768,8 @@ hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream
                        P.suffix, P.type, P.aux);
     return hipGetLastError();
 }
+
+#endif  // JL_STUDY
 
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st) {
     switch (P.mode) {

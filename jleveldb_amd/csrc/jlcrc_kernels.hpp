@@ -60,7 +60,7 @@ struct GV4Args {
     const uint32_t *n_rounds;   // device count of rounds (sorted pipeline)
     uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
     uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
-    uint32_t no_fast;           // study (JL_GV4_NOFAST): every ring turn takes the per-entry path
+    uint32_t study;             // study build only: crc_gv4_kernel variant (0 = the product kernel)
     uint32_t *parts;            // split blocks: raw chunk states (group idx = kGPart | part index)
 };
 // A block above kGSplitMin (MODE_CRC) is cut into m <= 2048 chunks of S bytes
@@ -90,11 +90,13 @@ struct LogEvent {  // layout-identical to jl_log_event
     uint16_t pad;
 };
 
+// study build only (JL_STUDY): the round-1 4 KiB kernels and the chunked general kernel
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
                           uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
                           hipStream_t st);
 // v4 fast path (fixed_v4.hip): lpb = lanes per block (8, 16); img = the v4 image for that lpb;
-// shape 0 = the default (16 ring slots, 1024 threads), 1..3 = occupancy study shapes
+// the product launches lpb 8, nt, shape 3 (8 ring slots, 1024 threads); the other
+// shapes exist in the study build only
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
                              int grid, int lpb, int nt, int shape, hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
@@ -133,6 +135,33 @@ hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, ui
 hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
                                LogEvent *ev, int checksum, uint64_t n_events, unsigned long long *firstbad,
                                hipStream_t st);
+// Fused log verification (log_stream.hip): one pass over the log, 8 lanes per
+// 32 KiB block and 8 blocks per wave; walks the headers from the streamed bytes
+// and folds every record's crc.  Per block: the events it walked (up to `cap`
+// in slots[b * cap ...], tentatively OK), their count and the index of the
+// first record whose crc failed.
+constexpr uint32_t kLSLaneByte = 32768u * 4u;   // must equal jlmath::kLS*Dword * 4
+constexpr uint32_t kLSShiftByte = 34816u * 4u;
+constexpr uint32_t kLSEByte = 35712u * 4u;
+constexpr uint32_t kLSMaskByte = 36224u * 4u;
+constexpr uint32_t kLSStageByte = 36384u * 4u;
+constexpr uint32_t kLSNone = 0xffffffffu;       // first_bad: no failure
+struct LogStreamArgs {
+    const uint8_t *log;
+    uint64_t size;
+    uint32_t n_blocks;
+    uint32_t cap;          // event slots per block
+    LogEvent *slots;       // n_blocks * cap
+    uint32_t *count;       // n_blocks: events walked
+    uint32_t *first_bad;   // n_blocks: slot of the first BAD_CRC record (kLSNone: none)
+    uint32_t *overflow;    // set when a block walked more than cap events
+};
+hipError_t launch_logstream(const void *img, const LogStreamArgs &A, int grid, hipStream_t st);
+// copies the walked events of every block to ev[start[b] ...] (at most cap_out in
+// all), applying first_bad: that record becomes BAD_CRC, later ones of its block
+// kind 0 (dropped with the rest of the 32 KiB block, J/db/LogReader.java:359-367)
+hipError_t launch_logstream_compact(const LogStreamArgs &A, const uint64_t *start, LogEvent *ev, uint64_t cap_out,
+                                    hipStream_t st);
 hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, const uint64_t *frag_hdr_off,
                            const uint32_t *frag_len, uint64_t n_frags, uint8_t *log, uint64_t *pay_off, hipStream_t st);
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st);

@@ -6,6 +6,9 @@
 
 #include "engine_device.hpp"
 
+#ifndef JL_STUDY
+#define JL_STUDY 0
+#endif
 #ifndef JL_MODE
 #error "compile with -DJL_MODE=<jlk::MODE_*>"
 #endif
@@ -399,10 +402,14 @@ drain:
 template <>
 hipError_t launch_stream_m<JL_MODE>(const void *img, const KParams &P, const uint64_t *part, int grid, int depth,
                                     hipStream_t st) {
-    if (P.dbg)
+#if JL_STUDY
+    if (P.dbg) {  // address-check build (JL_STREAM_DEBUG)
         hipLaunchKernelGGL((crc_stream_kernel<JL_MODE, 32, true>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P,
                            part);
-    else if (depth <= 16)
+        return hipGetLastError();
+    }
+#endif
+    if (depth <= 16)
         hipLaunchKernelGGL((crc_stream_kernel<JL_MODE, 16>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P, part);
     else if (depth <= 32)
         hipLaunchKernelGGL((crc_stream_kernel<JL_MODE, 32>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P, part);

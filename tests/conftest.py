@@ -39,6 +39,20 @@ def gpu(jl):
     return torch.device("cuda:0")
 
 
+@pytest.fixture
+def engine_options(jl):
+    """Sets engine options (jl_set_option) for one test and restores them after it."""
+    saved = {}
+
+    def set_(option, value):
+        prev = jl.set_option(option, value)
+        saved.setdefault(option, prev)
+
+    yield set_
+    for option, value in saved.items():
+        jl.set_option(option, value)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

@@ -17,7 +17,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "jleveldb_amd", "csrc")
 UNITS = ([("jlcrc_kernels.hip", []), ("fixed_v4.hip", [])] + [("stream_kernel.hip", [f"-DJL_MODE={m}"]) for m in range(5)]
-         + [("general_v4.hip", [f"-DJL_MODE={m}"]) for m in range(3)])
+         + [("general_v4.hip", [f"-DJL_MODE={m}"]) for m in range(3)] + [("log_stream.hip", [])])
 
 
 @pytest.fixture(scope="module")
@@ -27,8 +27,9 @@ def asm(tmp_path_factory):
     def one(i):
         src, defs = UNITS[i]
         out = d / f"u{i}.s"
+        # the study build: the product kernels and every superseded / debug variant
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed",
-                        "--cuda-device-only", "-S", *defs, "-o", str(out), os.path.join(CSRC, src)],
+                        "--cuda-device-only", "-S", "-DJL_STUDY=1", *defs, "-o", str(out), os.path.join(CSRC, src)],
                        check=True, capture_output=True)
         return out.read_text()
 
@@ -50,11 +51,14 @@ def test_no_stale_ring_reads(asm):
     assert sum("crc_stream_kernel" in s for s in ks) >= 15
     assert any("crc_fixed4k_x2" in s for s in ks) and any("crc_fixed4k_v4" in s for s in ks)
     assert sum("crc_gv4_kernel" in s for s in ks) >= 3
+    assert any("crc_logstream_kernel" in s for s in ks)
     branchy = ("crc_stream_kernel", "crc_general_kernel")
 
     def one(s, b):
         if "crc_gv4_kernel" in s:
             return check_pinned(b, first=216) + check_local(b)
+        if "crc_logstream_kernel" in s:  # ring pinned in v136..v167 (12 waves per CU)
+            return check_pinned(b, first=136, last=167) + check_local(b)
         return check_local(b) if any(k in s for k in branchy) else check(b)
 
     problems = {s: one(s, b) for s, b in ks.items()}

@@ -1,5 +1,5 @@
 """The general v4 kernel (general_v4.hip; the default general path except for
-small offset/length batches, JL_GENERAL=gv4 forces it) against the oracle: the variable-size, fixed-stride, table and log parity
+small offset/length batches; JL_OPT_GENERAL_PATH = JL_PATH_GV4 forces it) against the oracle: the variable-size, fixed-stride, table and log parity
 cases of test_gpu_parity.py re-run with it selected, plus cases aimed at its
 sorted-round pipeline (every K bucket, partial rounds, empty blocks mixed in,
 blocks around the 128-B step grid, a block above the solo threshold)."""
@@ -13,8 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def gv4_kernel(monkeypatch):
-    monkeypatch.setenv("JL_GENERAL", "gv4")
+def gv4_kernel(jl, engine_options):
+    engine_options(jl.OPT_GENERAL_PATH, jl.PATH_GV4)
 
 
 def test_gv4_every_length_and_alignment(gpu, jl, oracle):
@@ -102,9 +102,9 @@ def test_gv4_log(gpu, jl, oracle, golden):
     base.test_log_dev_resident(gpu, jl, oracle)
 
 
-def test_log_through_stream_kernel(gpu, jl, oracle, golden, monkeypatch):
-    """The log verify defaults to gv4; the stream kernel (JL_GENERAL=stream) stays covered."""
-    monkeypatch.setenv("JL_GENERAL", "stream")
+def test_log_through_stream_kernel(gpu, jl, oracle, golden, engine_options):
+    """The log verify's batched crc defaults to gv4; the stream kernel stays covered."""
+    engine_options(jl.OPT_GENERAL_PATH, jl.PATH_STREAM)
     test_gv4_log(gpu, jl, oracle, golden)
 
 
@@ -122,10 +122,10 @@ def test_gv4_fixed_unaligned_base(gpu, jl, oracle, shift, block_bytes):
 
 
 @pytest.mark.parametrize("case", ["every_length", "zipf", "table"])
-def test_stream_kernel_still_exact(gpu, jl, oracle, golden, monkeypatch, case):
+def test_stream_kernel_still_exact(gpu, jl, oracle, golden, engine_options, case):
     """The stream kernel (the default for small offset/length batches) on the
     cases above, forced."""
-    monkeypatch.setenv("JL_GENERAL", "stream")
+    engine_options(jl.OPT_GENERAL_PATH, jl.PATH_STREAM)
     if case == "every_length":
         base.test_batch_every_length_and_alignment(gpu, jl, oracle)
     elif case == "zipf":
@@ -155,14 +155,14 @@ def test_gv4_rounds_pipeline_large_bins(gpu, jl, oracle):
 
 
 @pytest.mark.parametrize("part_cap", [None, "8"])
-def test_gv4_split_blocks(gpu, jl, oracle, monkeypatch, part_cap):
+def test_gv4_split_blocks(gpu, jl, oracle, engine_options, part_cap):
     """Blocks above 512 KiB are split into chunks (computed from state 0 on their
     own waves) and folded per block with z^len: lengths around the split
     threshold and the chunk size, an 8 MiB + 77 block, a 40 MiB block (160
     chunks), unaligned starts, with init / suffix / unmasked variants.
     part_cap 8: only the first split blocks get chunk slots, the rest stay whole."""
     if part_cap:
-        monkeypatch.setenv("JL_GV4_PARTCAP", part_cap)
+        engine_options(jl.OPT_SPLIT_CAP, int(part_cap))
     rng = np.random.default_rng(25)
     lens = np.array([(512 << 10) + 1, (512 << 10), 600 << 10, (1 << 20) + 3, (768 << 10), (8 << 20) + 77, 40 << 20,
                      5, 4096, 0, (256 << 10) * 3 - 1], np.uint32)

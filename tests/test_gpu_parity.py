@@ -42,10 +42,14 @@ FIXED_VARIANTS = {"x2": "3", "x2plain": "2", "v4_8": "7", "v4_16": "8", "v4_8_pl
 
 @pytest.mark.parametrize("variant", sorted(FIXED_VARIANTS))
 @pytest.mark.parametrize("n_blocks", [1, 7, 8, 9, 63, 64, 65, 1000, 16385, 65536 + 13])
-def test_fixed_4k_kernel_variants(gpu, jl, oracle, monkeypatch, variant, n_blocks):
-    """Every 4 KiB kernel variant (JL_FIXED_CHAINS), ragged counts around the
-    round (8/4 blocks), group (64 blocks) and grid boundaries."""
-    monkeypatch.setenv("JL_FIXED_CHAINS", FIXED_VARIANTS[variant])
+def test_fixed_4k_kernel_variants(gpu, jl, oracle, engine_options, variant, n_blocks):
+    """The 4 KiB product kernel (v4_8) — and in a study build (make STUDY=1) every
+    superseded variant (JL_OPT_FIXED_KERNEL) — at ragged counts around the round
+    (8/4 blocks), group (64 blocks) and grid boundaries."""
+    if variant != "v4_8":
+        if "study build" not in jl.version():
+            pytest.skip("superseded 4 KiB kernel: study build only")
+        engine_options(jl.OPT_FIXED_KERNEL, int(FIXED_VARIANTS[variant]))
     rng = np.random.default_rng(1000 + n_blocks)
     host = rng.integers(0, 256, n_blocks * 4096, dtype=np.uint8)
     d = to_dev(host, gpu)
@@ -54,9 +58,8 @@ def test_fixed_4k_kernel_variants(gpu, jl, oracle, monkeypatch, variant, n_block
         assert np.array_equal(got, oracle.fixed(host, 4096, n_blocks, flags=flags, threads=THREADS)), flags
 
 
-def test_fixed_4k_v4_out_of_place_views(gpu, jl, oracle, monkeypatch):
+def test_fixed_4k_v4_out_of_place_views(gpu, jl, oracle):
     """v4 kernel on a sub-view (unaligned-to-group base, block count not a round multiple)."""
-    monkeypatch.setenv("JL_FIXED_CHAINS", "7")
     rng = np.random.default_rng(77)
     host = rng.integers(0, 256, 300 * 4096, dtype=np.uint8)
     d = to_dev(host, gpu)
@@ -113,12 +116,12 @@ def test_batch_every_length_and_alignment(gpu, jl, oracle):
 
 
 @pytest.mark.parametrize("depth,partition", [("32", True), ("48", False), ("16", False)])
-def test_stream_depths_and_partition(gpu, jl, oracle, monkeypatch, depth, partition):
-    """Stream-kernel ring depths (JL_STREAM_DEPTH) and the count split (JL_NO_PARTITION)."""
-    monkeypatch.setenv("JL_GENERAL", "stream")
-    monkeypatch.setenv("JL_STREAM_DEPTH", depth)
+def test_stream_depths_and_partition(gpu, jl, oracle, engine_options, depth, partition):
+    """Stream-kernel ring depths (JL_OPT_STREAM_DEPTH) and the count split (JL_OPT_STREAM_PARTITION 0)."""
+    engine_options(jl.OPT_GENERAL_PATH, jl.PATH_STREAM)
+    engine_options(jl.OPT_STREAM_DEPTH, int(depth))
     if not partition:
-        monkeypatch.setenv("JL_NO_PARTITION", "1")
+        engine_options(jl.OPT_STREAM_PARTITION, 0)
     test_batch_every_length_and_alignment(gpu, jl, oracle)
     test_batch_large_and_zipf(gpu, jl, oracle)
 
