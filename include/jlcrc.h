@@ -190,16 +190,20 @@ typedef struct jl_log_event {
  * verifies every record's masked CRC (crc over type || payload, LogWriter.java:147)
  * and truncates each block after its first failure, exactly as the reference
  * reader clears its buffer.  Writes up to `cap` events to d_events and the total
- * to *n_events (host pointer; this call synchronises on the stream once, at the end).
+ * to *n_events (host pointer; this call synchronises on the stream).
  * `checksum` (LogReader's checksum flag, J/db/LogReader.java:356):
- *   JL_LOG_NO_CHECKSUM  header walk only, every record accepted;
- *   JL_LOG_CHECKSUM     one fused pass over the bytes (walk + crc, log_stream.hip);
- *                       blocks of more than 256 records take the two-pass path;
- *   JL_LOG_CHECKSUM_TWO_PASS  header walk, then a batched crc of the records
- *                       (same results; kept as the fused path's cross-check). */
+ *   JL_LOG_NO_CHECKSUM     header walk only, every record accepted;
+ *   JL_LOG_CHECKSUM        header walk kernel, then the records' masked crcs as
+ *                          one batch through the general v4 kernel (the default);
+ *   JL_LOG_CHECKSUM_TWO_PASS  the same path (explicit name);
+ *   JL_LOG_CHECKSUM_FUSED  one pass over the bytes that walks and verifies
+ *                          together (log_stream.hip); same results, slower on
+ *                          short records; blocks of more than 256
+ *                          records fall back to the two-pass path. */
 #define JL_LOG_NO_CHECKSUM 0
 #define JL_LOG_CHECKSUM 1
 #define JL_LOG_CHECKSUM_TWO_PASS 2
+#define JL_LOG_CHECKSUM_FUSED 3
 int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                       uint64_t *n_events, void *stream);
 /* Host-memory form (log = the on-disk .log / MANIFEST bytes); blocking. */

@@ -24,8 +24,8 @@ FLAG_MASK = 1
 
 # jl_log_event kinds (include/jlcrc.h)
 LOG_OK, LOG_BAD_CRC, LOG_BAD_LENGTH, LOG_ZERO_SKIP, LOG_EOF_BAD_LENGTH, LOG_EOF_TRUNC = 1, 2, 3, 4, 5, 6
-# checksum argument of the log entry points (include/jlcrc.h): False/0, True/1 (fused single pass), 2 (two-pass)
-LOG_NO_CHECKSUM, LOG_CHECKSUM, LOG_CHECKSUM_TWO_PASS = 0, 1, 2
+# checksum argument of the log entry points (include/jlcrc.h): False/0, True/1 (= 2, two-pass), 3 (fused single pass)
+LOG_NO_CHECKSUM, LOG_CHECKSUM, LOG_CHECKSUM_TWO_PASS, LOG_CHECKSUM_FUSED = 0, 1, 2, 3
 LOG_EVENT_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u4"), ("type", "u1"), ("kind", "u1"), ("pad", "<u2")])
 LOG_RECORD_DTYPE = np.dtype([("offset", "<u8"), ("arena_off", "<u8"), ("size", "<u8")])
 LOG_REPORT_DTYPE = np.dtype([("bytes", "<u8"), ("reason", "<u4"), ("aux", "<u4")])

@@ -49,16 +49,47 @@
 #error "compile with -DJL_MODE=<jlk::MODE_*>"
 #endif
 #ifndef JL_GV4_THREADS
-#define JL_GV4_THREADS 512  // 8 waves per CU: 256 VGPRs per lane for the ring + cursors
+#define JL_GV4_THREADS 1024  // 16 waves per CU: 128 VGPRs per lane, 40 of them pinned
 #endif
 
 namespace jlk {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-// the 8 ring slots: (slot, register quad, its 4 registers), pinned in v224..v255
-#define JL_GV4_RING 8
-#define JL_GV4_VGPR_BUDGET 216  // v216..v223: the two round-descriptor sets, v224..v255: the ring
+// The pinned registers: two round-descriptor sets (JL_GV4_DQ0/1) and the 8
+// ring slots (slot, register quad, its 4 registers), the top 40 VGPRs a wave of
+// this shape may use: v88..v127 at 16 waves per CU (1024 threads, 128 VGPRs),
+// v216..v255 at 8 waves (512 threads).  The compiler allocates about 65 VGPRs
+// below them; tests/test_asm.py rejects any compiler instruction touching them.
+#if JL_GV4_THREADS == 1024
+#define JL_GV4_PIN_FIRST 88
+#define JL_GV4_SLOTS(X) \
+    X(0, "v[96:99]", "v96", "v97", "v98", "v99") \
+    X(1, "v[100:103]", "v100", "v101", "v102", "v103") \
+    X(2, "v[104:107]", "v104", "v105", "v106", "v107") \
+    X(3, "v[108:111]", "v108", "v109", "v110", "v111") \
+    X(4, "v[112:115]", "v112", "v113", "v114", "v115") \
+    X(5, "v[116:119]", "v116", "v117", "v118", "v119") \
+    X(6, "v[120:123]", "v120", "v121", "v122", "v123") \
+    X(7, "v[124:127]", "v124", "v125", "v126", "v127")
+#define JL_GV4_SLOTS_LO(X) \
+    X(0, "v[96:99]", "v96", "v97", "v98", "v99") \
+    X(1, "v[100:103]", "v100", "v101", "v102", "v103") \
+    X(2, "v[104:107]", "v104", "v105", "v106", "v107") \
+    X(3, "v[108:111]", "v108", "v109", "v110", "v111")
+#define JL_GV4_SLOTS_HI(X) \
+    X(4, "v[112:115]", "v112", "v113", "v114", "v115") \
+    X(5, "v[116:119]", "v116", "v117", "v118", "v119") \
+    X(6, "v[120:123]", "v120", "v121", "v122", "v123") \
+    X(7, "v[124:127]", "v124", "v125", "v126", "v127")
+#define JL_GV4_DQ0 "v[88:91]"
+#define JL_GV4_DR0 "v88", "v89", "v90", "v91"
+#define JL_GV4_DMOV0 "v_mov_b32 %0, v88\n\tv_mov_b32 %1, v89\n\tv_mov_b32 %2, v90\n\tv_mov_b32 %3, v91"
+#define JL_GV4_DQ1 "v[92:95]"
+#define JL_GV4_DR1 "v92", "v93", "v94", "v95"
+#define JL_GV4_DMOV1 "v_mov_b32 %0, v92\n\tv_mov_b32 %1, v93\n\tv_mov_b32 %2, v94\n\tv_mov_b32 %3, v95"
+#elif JL_GV4_THREADS == 512
+#define JL_GV4_PIN_FIRST 216
 #define JL_GV4_SLOTS(X) \
     X(0, "v[224:227]", "v224", "v225", "v226", "v227") \
     X(1, "v[228:231]", "v228", "v229", "v230", "v231") \
@@ -68,7 +99,6 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     X(5, "v[244:247]", "v244", "v245", "v246", "v247") \
     X(6, "v[248:251]", "v248", "v249", "v250", "v251") \
     X(7, "v[252:255]", "v252", "v253", "v254", "v255")
-// the two half turns (slots 0..3 and 4..7)
 #define JL_GV4_SLOTS_LO(X) \
     X(0, "v[224:227]", "v224", "v225", "v226", "v227") \
     X(1, "v[228:231]", "v228", "v229", "v230", "v231") \
@@ -79,6 +109,16 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     X(5, "v[244:247]", "v244", "v245", "v246", "v247") \
     X(6, "v[248:251]", "v248", "v249", "v250", "v251") \
     X(7, "v[252:255]", "v252", "v253", "v254", "v255")
+#define JL_GV4_DQ0 "v[216:219]"
+#define JL_GV4_DR0 "v216", "v217", "v218", "v219"
+#define JL_GV4_DMOV0 "v_mov_b32 %0, v216\n\tv_mov_b32 %1, v217\n\tv_mov_b32 %2, v218\n\tv_mov_b32 %3, v219"
+#define JL_GV4_DQ1 "v[220:223]"
+#define JL_GV4_DR1 "v220", "v221", "v222", "v223"
+#define JL_GV4_DMOV1 "v_mov_b32 %0, v220\n\tv_mov_b32 %1, v221\n\tv_mov_b32 %2, v222\n\tv_mov_b32 %3, v223"
+#else
+#error "JL_GV4_THREADS: 512 or 1024"
+#endif
+#define JL_GV4_RING 8
 
 template <int MODE>
 struct GV4 {
@@ -144,7 +184,7 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, ui
 }
 
 // Round descriptors prefetched with a VECTOR load into one of two pinned register
-// sets (v216..v219 / v220..v223, each lane its group's 16-B GDesc), touched only
+// sets (JL_GV4_DQ0 / JL_GV4_DQ1, each lane its group's 16-B GDesc), touched only
 // by inline asm like the ring.  The prefetch cursor issues round k+1's load when
 // it starts round k, if round k has >= P entries: the ring's own waits then
 // cover it before either cursor reads it (at least P-1 younger ring loads), and
@@ -155,17 +195,17 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, ui
 __device__ __forceinline__ void desc_issue(const GV4Args &A, uint32_t r, uint32_t q, uint32_t set) {
     const uint64_t a = (uint64_t)(uintptr_t)(A.desc + (uint64_t)r * 8u + q);
     if (set)
-        asm volatile("global_load_dwordx4 v[220:223], %0, off" ::"v"(a) : "memory", "v220", "v221", "v222", "v223");
+        asm volatile("global_load_dwordx4 " JL_GV4_DQ1 ", %0, off" ::"v"(a) : "memory", JL_GV4_DR1);
     else
-        asm volatile("global_load_dwordx4 v[216:219], %0, off" ::"v"(a) : "memory", "v216", "v217", "v218", "v219");
+        asm volatile("global_load_dwordx4 " JL_GV4_DQ0 ", %0, off" ::"v"(a) : "memory", JL_GV4_DR0);
 }
 __device__ __forceinline__ RoundView desc_read(uint32_t set) {
     uint32_t lo, hi, ix, k;
     if (set)
-        asm volatile("v_mov_b32 %0, v220\n\tv_mov_b32 %1, v221\n\tv_mov_b32 %2, v222\n\tv_mov_b32 %3, v223"
+        asm volatile(JL_GV4_DMOV1
                      : "=v"(lo), "=v"(hi), "=v"(ix), "=v"(k));
     else
-        asm volatile("v_mov_b32 %0, v216\n\tv_mov_b32 %1, v217\n\tv_mov_b32 %2, v218\n\tv_mov_b32 %3, v219"
+        asm volatile(JL_GV4_DMOV0
                      : "=v"(lo), "=v"(hi), "=v"(ix), "=v"(k));
     // empty groups of a partial round mirror group 0 (lane 0)
     const bool nul = ix == kGNull;
@@ -297,7 +337,7 @@ struct GPF {
 // debugging), 2 = ring loads without nt (cache-policy study), 3 = whole 8-entry
 // fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study)
 template <int MODE, int VAR = 0>
-__global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_GV4_VGPR_BUDGET))) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
+__global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
     constexpr int P_ = JL_GV4_RING;
     constexpr bool DBG = VAR == 4;  // JL_GV4_DEBUG builds the address checks in
@@ -324,9 +364,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) __attribute__((amdgpu_num_vgpr(JL_G
 
     GPF<MODE, DBG> pf;
     pf.init(A, cr, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
-    // The ring lives in PINNED registers v224..v255 (slot u = v[224+4u : 227+4u]),
-    // above the compiler's budget (amdgpu_num_vgpr(216); v216..v223 hold the two
-    // prefetched round-descriptor sets): the register allocator
+    // The ring lives in PINNED registers (JL_GV4_SLOTS, the two prefetched
+    // round-descriptor sets JL_GV4_DQ0/1 just below it), above what the
+    // compiler allocates: the register allocator
     // can never copy, reuse or spill a slot while its load is in flight — with
     // compiler-allocated ring values this kernel's branchy rounds made it do that
     // (r1: intermittent faults).  Each slot is touched only by inline asm: the

@@ -800,7 +800,7 @@ static int log_verify_stream(const void *d_log, uint64_t log_bytes, jl_log_event
 static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                            uint64_t *n_events, hipStream_t st) {
     Context &c = ctx();
-    if (checksum == 1) {  // JL_LOG_CHECKSUM: the fused single-pass path, unless a block overflows its slots
+    if (checksum == JL_LOG_CHECKSUM_FUSED) {  // the single-pass kernel, unless a block overflows its slots
         bool fallback = false;
         *n_events = 0;
         if (log_bytes == 0) return JL_OK;
@@ -851,6 +851,7 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
                       uint64_t *n_events, void *stream) {
     if (int r = ensure_ready()) return r;
     if (!n_events || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev: null pointer");
+    if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify_dev: bad checksum mode");
     Context &c = ctx();
     std::lock_guard<std::mutex> lk(c.mu);  // shares the walk workspace
     return log_verify_impl(d_log, log_bytes, checksum, d_events, cap, n_events, pick(stream));
@@ -860,6 +861,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
                   uint64_t *n_events) {
     if (int r = ensure_ready()) return r;
     if (!n_events || (log_bytes && !log)) return fail(JL_ERR_INVALID, "jl_log_verify: null pointer");
+    if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify: bad checksum mode");
     Context &c = ctx();
     std::lock_guard<std::mutex> lk(c.mu);
     hipStream_t st = c.stream;

@@ -56,7 +56,7 @@ def test_no_stale_ring_reads(asm):
 
     def one(s, b):
         if "crc_gv4_kernel" in s:
-            return check_pinned(b, first=216) + check_local(b)
+            return check_pinned(b, first=88, last=127) + check_local(b)  # 1024 threads: v88..v127
         if "crc_logstream_kernel" in s:  # ring pinned in v136..v167 (12 waves per CU)
             return check_pinned(b, first=136, last=167) + check_local(b)
         return check_local(b) if any(k in s for k in branchy) else check(b)

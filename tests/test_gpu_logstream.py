@@ -1,4 +1,4 @@
-"""The fused log-verify path (jleveldb_amd/csrc/log_stream.hip, JL_LOG_CHECKSUM)
+"""The fused log-verify path (jleveldb_amd/csrc/log_stream.hip, JL_LOG_CHECKSUM_FUSED)
 against the oracle's LogReader.readPhysicalRecord walk (J/db/LogReader.java:297-383)
 and against the engine's two-pass path (JL_LOG_CHECKSUM_TWO_PASS: walk kernel +
 batched crc), event for event.
@@ -17,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-FUSED, TWO_PASS = 1, 2
+FUSED, TWO_PASS = 3, 2
 
 
 def _live(ev):
