@@ -111,13 +111,17 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
 #define JL_STREAM_CHUNK_BYTES (64ull << 20)
 
 /* Arbitrary blocks in one arena: block i = d_base[d_off[i], d_off[i]+d_len[i]).
+ * base_bytes: the arena's size; a block reaching past it is not read and gets
+ *   the result 0 (descriptors are checked on the device, so a corrupt handle is
+ *   never an out-of-bounds HBM read).
  * d_init (nullable): per-block initial crc as in Crc32C.extend(init, ...),
  *   J/util/Crc32C.java:43-48 (LogWriter uses typeCrc[t], J/db/LogWriter.java:147).
  * d_suffix (nullable): one extra byte appended after each block, as
  *   TableBuilder.writeRawBlock appends the type byte, J/table/TableBuilder.java:313-315.
  * d_out[i] = crc (or mask(crc) with JL_FLAG_MASK). */
-int jl_crc32c_batch_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint32_t *d_init,
-                        const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out, void *stream);
+int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                        const uint32_t *d_init, const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out,
+                        void *stream);
 
 /* Host-memory form of jl_crc32c_batch_dev: stages base[0, base_bytes) and the
  * descriptors through pinned buffers to the device, runs the kernel, copies the
@@ -135,11 +139,13 @@ int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint3
 
 /* Read side, batched TableFormat.readBlock checksum test
  * (J/table/TableFormat.java:207-218): for handle i (offset d_off[i], size
- * d_size[i]; the block plus its trailer must lie inside the file) sets
- * d_status[i] = 1 when unmask(LE32 @ off+size+1) == crc32c(file[off, off+size+1)),
- * else 0 ("block checksum mismatch"). */
-int jl_table_verify_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, uint64_t n,
-                        uint8_t *d_status, void *stream);
+ * d_size[i]) sets d_status[i] = 1 when
+ * unmask(LE32 @ off+size+1) == crc32c(file[off, off+size+1)), else 0 ("block
+ * checksum mismatch").  A handle whose block and 5-byte trailer do not lie
+ * inside [0, file_bytes) gets 0 and nothing past the file is read (checked on
+ * the device: the handles may come from untrusted index blocks). */
+int jl_table_verify_dev(const void *d_file, uint64_t file_bytes, const uint64_t *d_off, const uint32_t *d_size,
+                        uint64_t n, uint8_t *d_status, void *stream);
 /* Block handles of a whole SSTable image (host, no device work): parses the
  * footer (TableFormat.Footer.decodeFrom, J/table/TableFormat.java:126-146), the
  * index block's entries (Block.decodeEntry, J/table/Block.java:312-342; values

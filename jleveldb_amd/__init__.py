@@ -82,11 +82,11 @@ def lib() -> ctypes.CDLL:
         "jl_set_option": (i32, [i32, ctypes.c_int64]),
         "jl_get_option": (ctypes.c_int64, [i32]),
         "jl_crc32c_fixed_dev": (i32, [vp, u64, u64, u32, vp, vp]),
-        "jl_crc32c_batch_dev": (i32, [vp, vp, vp, vp, vp, u64, u32, vp, vp]),
+        "jl_crc32c_batch_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, u32, vp, vp]),
         "jl_crc32c_fixed": (i32, [vp, u64, u64, u32, vp]),
         "jl_crc32c_batch": (i32, [vp, u64, vp, vp, vp, vp, u64, u32, vp]),
         "jl_table_trailers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
-        "jl_table_verify_dev": (i32, [vp, vp, vp, u64, vp, vp]),
+        "jl_table_verify_dev": (i32, [vp, u64, vp, vp, u64, vp, vp]),
         "jl_table_verify": (i32, [vp, u64, vp, vp, u64, vp]),
         "jl_table_block_handles": (i32, [vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_verify_dev": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64), vp]),
@@ -272,7 +272,8 @@ def crc32c_batch_dev(base, off, length, init=None, suffix=None, flags: int = FLA
     n = off.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    _check(lib().jl_crc32c_batch_dev(_dptr(base), _dptr(off), _dptr(length), _dptr(init), _dptr(suffix), n, flags,
+    _check(lib().jl_crc32c_batch_dev(_dptr(base), base.numel(), _dptr(off), _dptr(length), _dptr(init), _dptr(suffix),
+                                     n, flags,
                                      _dptr(out), _stream(stream)), "jl_crc32c_batch_dev")
     return out
 
@@ -341,7 +342,8 @@ def table_verify_dev(file, off, size, out=None, stream=None):
     n = off.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.uint8, device=file.device)
-    _check(lib().jl_table_verify_dev(_dptr(file), _dptr(off), _dptr(size), n, _dptr(out), _stream(stream)),
+    _check(lib().jl_table_verify_dev(_dptr(file), file.numel(), _dptr(off), _dptr(size), n, _dptr(out),
+                                     _stream(stream)),
            "jl_table_verify_dev")
     return out
 

@@ -720,13 +720,21 @@ __device__ __forceinline__ void gv4_chunk(uint64_t n, uint64_t &i0, uint64_t &i1
 
 // bin of block i (0xffffffff: empty block, whose result is written here:
 // extend(init, empty) = init, then the suffix byte)
+__device__ __forceinline__ bool gv4_in_range(const KParams &P, uint64_t i) {
+    return !P.off || block_in_range(P, P.off[i], P.len[i] + P.len_add);
+}
+
 __device__ __forceinline__ uint32_t gv4_bin(const KParams &P, uint64_t i, bool write_empty) {
     uint64_t p;
     uint32_t n;
     gv4_block(P, i, p, n);
-    const uint32_t K = gv4_K(p, n);
+    const bool bad = !gv4_in_range(P, i);
+    const uint32_t K = bad ? 0u : gv4_K(p, n);
     if (K) return K < kGSoloKey ? K : kGSoloKey;
-    if (write_empty) {
+    if (write_empty && bad) {  // a descriptor past the caller's bytes: nothing read, result 0
+        if (P.mode == MODE_CRC) P.out32[i] = 0u;
+        else P.out8[i] = 0u;
+    } else if (write_empty) {
         uint32_t st = ~(P.init ? P.init[i] : 0u);
         if (P.suffix) st = (st >> 8) ^ P.aux[(st ^ P.suffix[i]) & 0xffu];
         const uint32_t crc = ~st;
@@ -779,7 +787,7 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uin
             uint32_t n, cs, m;
             gv4_block(P, i, p, n);
             bool split = false;
-            if (gv4_split_geom(P, S, n, cs, m)) {  // rare: blocks > 512 KiB
+            if (gv4_in_range(P, i) && gv4_split_geom(P, S, n, cs, m)) {  // rare: blocks > 512 KiB
                 const unsigned long long base = atomicAdd(&S.ctl[0], (unsigned long long)m);
                 split = base + m <= S.part_cap;
                 S.bigbase[i] = split ? (uint32_t)base : 0xffffffffu;
@@ -898,7 +906,9 @@ __global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, GSplit S, co
             uint64_t p;
             uint32_t n, cs, m;
             gv4_block(P, i, p, n);
-            bin[k] = gv4_split_geom(P, S, n, cs, m) && S.bigbase[i] != 0xffffffffu ? kSplitBin : gv4_bin(P, i, false);
+            bin[k] = gv4_in_range(P, i) && gv4_split_geom(P, S, n, cs, m) && S.bigbase[i] != 0xffffffffu
+                         ? kSplitBin
+                         : gv4_bin(P, i, false);
         }
         rank[k] = wave_rank(bin[k] == kSplitBin ? 0xffffffffu : bin[k], h, cursor);
     }

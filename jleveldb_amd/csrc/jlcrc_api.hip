@@ -136,6 +136,7 @@ jlk::KParams base_params(const void *d_base, uint64_t n, int mode) {
     P.zero = ctx().d_zero;
     P.n = n;
     P.mode = mode;
+    P.base_bytes = ~0ull;
     return P;
 }
 
@@ -590,12 +591,14 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     return JL_OK;
 }
 
-int jl_crc32c_batch_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint32_t *d_init,
-                        const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out, void *stream) {
+int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t *d_off, const uint32_t *d_len,
+                        const uint32_t *d_init, const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out,
+                        void *stream) {
     if (int r = ensure_ready()) return r;
     if (n == 0) return JL_OK;
     if (!d_base || !d_off || !d_len || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_batch_dev: null pointer");
     jlk::KParams P = base_params(d_base, n, jlk::MODE_CRC);
+    P.base_bytes = base_bytes;
     P.off = d_off;
     P.len = d_len;
     P.init = d_init;
@@ -657,12 +660,13 @@ int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint3
     return run_general(P, pick(stream));
 }
 
-int jl_table_verify_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, uint64_t n,
-                        uint8_t *d_status, void *stream) {
+int jl_table_verify_dev(const void *d_file, uint64_t file_bytes, const uint64_t *d_off, const uint32_t *d_size,
+                        uint64_t n, uint8_t *d_status, void *stream) {
     if (int r = ensure_ready()) return r;
     if (n == 0) return JL_OK;
     if (!d_file || !d_off || !d_size || !d_status) return fail(JL_ERR_INVALID, "jl_table_verify_dev: null pointer");
     jlk::KParams P = base_params(d_file, n, jlk::MODE_TABLE_VERIFY);
+    P.base_bytes = file_bytes;
     P.off = d_off;
     P.len = d_size;
     P.len_add = 1;  // block || type byte

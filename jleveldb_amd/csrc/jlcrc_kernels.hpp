@@ -41,6 +41,10 @@ struct KParams {
     uint32_t *out32;
     uint8_t *out8;
     const uint64_t *hdr_off;  // MODE_LOG_HEADER: header i goes to out8 + hdr_off[i] (null: out8 + 7*i)
+    // caller-supplied bytes at `base` (~0: unchecked, the engine's own descriptors):
+    // a block (plus, for MODE_TABLE_VERIFY, its stored crc) reaching past it is
+    // not read; its result is 0 (crc 0 / verify "mismatch")
+    uint64_t base_bytes;
     // debug bounds checking (JL_STREAM_DEBUG): valid load range and a log of
     // offending accesses {block, entry, lane, address}; dbg == null: off
     uint64_t dbg_lo, dbg_hi;
@@ -81,6 +85,14 @@ struct GSplit {       // rounds-pipeline state of the block split
     uint32_t part_cap;  // parts[] capacity (blocks beyond it stay whole)
 };
 constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
+
+// block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)
+// inside the caller's base_bytes
+__host__ __device__ inline bool block_in_range(const KParams &P, uint64_t off, uint32_t n) {
+    if (P.base_bytes == ~0ull) return true;
+    const uint64_t need = (uint64_t)n + (P.mode == MODE_TABLE_VERIFY ? 4u : 0u);
+    return off <= P.base_bytes && need <= P.base_bytes - off;
+}
 
 struct LogEvent {  // layout-identical to jl_log_event
     uint64_t offset;

@@ -44,6 +44,7 @@ struct SDesc {
     uint32_t K;    // 256-B steps
     uint32_t f;    // 256K - n
     uint32_t ex;   // 1: an extra entry precedes the steps
+    uint32_t bad;  // 1: the block lies outside the caller's base_bytes (nothing read, result 0)
 };
 
 template <int MODE>
@@ -58,6 +59,8 @@ __device__ __forceinline__ SDesc stream_desc(const KParams &P, uint64_t i) {
         off = i * P.fixed_bytes;
         n = (uint32_t)P.fixed_bytes;
     }
+    d.bad = block_in_range(P, off, n) ? 0u : 1u;
+    if (d.bad) n = 0u;
     d.ptr = (uint64_t)(uintptr_t)P.base + off;
     d.n = n;
     d.K = (n + 255u) >> 8;
@@ -248,6 +251,7 @@ __device__ __forceinline__ void stream_result(const KParams &P, StreamFin &F, ui
             F.hhi = lane == F.nfin ? (uint32_t)(h >> 32) : F.hhi;
         }
     }
+    if (d.bad) r = 0u;
     F.res = lane == F.nfin ? r : F.res;
     F.aux = lane == F.nfin ? a : F.aux;
     if (++F.nfin == 64u) stream_flush<MODE>(P, F, lane);

@@ -7,12 +7,15 @@
  * (static natives) used by the patched Crc32C statics and by the batching shim
  * at the four call sites, see INTEGRATION.md.
  *
- * Heap arrays are pinned with GetPrimitiveArrayCritical for the duration of the
- * call (the C-ABI never retains pointers); direct ByteBuffers (mmap'd .ldb /
- * .log regions) are passed zero-copy via GetDirectBufferAddress.
+ * The scalar statics (host work of a few microseconds) pin their heap array with
+ * GetPrimitiveArrayCritical for the call only; the batch entry points that do
+ * device work copy heap arrays in and out instead, so no JVM array stays pinned
+ * across a kernel.  Direct ByteBuffers (mmap'd .ldb / .log regions) are passed
+ * zero-copy via GetDirectBufferAddress (the C-ABI never retains pointers).
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/jlcrc.h"
 
@@ -73,7 +76,10 @@ JNIEXPORT jstring JNICALL JFN(lastError)(JNIEnv *env, jclass cls) {
 }
 
 /* Batched TableFormat.readBlock checksum test over an mmap'd table (direct
- * ByteBuffer): status[i] = 1 ok / 0 "block checksum mismatch". */
+ * ByteBuffer): status[i] = 1 ok / 0 "block checksum mismatch".  The handle
+ * arrays are copied out (Get*ArrayRegion) and the statuses copied back: no JVM
+ * array stays pinned (GetPrimitiveArrayCritical would stall the collector)
+ * across the device work. */
 JNIEXPORT jint JNICALL JFN(tableVerify)(JNIEnv *env, jclass cls, jobject file, jlongArray off, jintArray size,
                                          jbyteArray status) {
     (void)cls;
@@ -84,13 +90,19 @@ JNIEXPORT jint JNICALL JFN(tableVerify)(JNIEnv *env, jclass cls, jobject file, j
         throw_(env, "java/lang/IllegalArgumentException", "tableVerify arguments");
         return JL_ERR_INVALID;
     }
-    jlong *o = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
-    jint *s = (*env)->GetPrimitiveArrayCritical(env, size, NULL);
-    jbyte *st = (*env)->GetPrimitiveArrayCritical(env, status, NULL);
-    int r = jl_table_verify(f, (uint64_t)cap, (const uint64_t *)o, (const uint32_t *)s, (uint64_t)n, (uint8_t *)st);
-    (*env)->ReleasePrimitiveArrayCritical(env, status, st, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, size, s, JNI_ABORT);
-    (*env)->ReleasePrimitiveArrayCritical(env, off, o, JNI_ABORT);
+    uint64_t *o = malloc((size_t)n * 8 + 1);
+    uint32_t *s = malloc((size_t)n * 4 + 1);
+    uint8_t *st = malloc((size_t)n + 1);
+    int r = JL_ERR_NOMEM;
+    if (o && s && st) {
+        (*env)->GetLongArrayRegion(env, off, 0, n, (jlong *)o);
+        (*env)->GetIntArrayRegion(env, size, 0, n, (jint *)s);
+        r = jl_table_verify(f, (uint64_t)cap, o, s, (uint64_t)n, st);
+        if (r == JL_OK) (*env)->SetByteArrayRegion(env, status, 0, n, (const jbyte *)st);
+    }
+    free(st);
+    free(s);
+    free(o);
     return r;
 }
 
@@ -109,13 +121,21 @@ JNIEXPORT jlong JNICALL JFN(tableBlockHandles)(JNIEnv *env, jclass cls, jobject 
         return JL_ERR_INVALID;
     }
     uint64_t got = 0;
-    jlong *o = (*env)->GetPrimitiveArrayCritical(env, off, NULL);
-    jint *s = (*env)->GetPrimitiveArrayCritical(env, size, NULL);
-    jbyte *k = (*env)->GetPrimitiveArrayCritical(env, kind, NULL);
-    int r = jl_table_block_handles(f, (uint64_t)cap, (uint64_t *)o, (uint32_t *)s, (uint8_t *)k, (uint64_t)n, &got);
-    (*env)->ReleasePrimitiveArrayCritical(env, kind, k, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, size, s, 0);
-    (*env)->ReleasePrimitiveArrayCritical(env, off, o, 0);
+    uint64_t *o = malloc((size_t)n * 8 + 1);
+    uint32_t *s = malloc((size_t)n * 4 + 1);
+    uint8_t *k = malloc((size_t)n + 1);
+    int r = JL_ERR_NOMEM;
+    if (o && s && k) {
+        r = jl_table_block_handles(f, (uint64_t)cap, o, s, k, (uint64_t)n, &got);
+        if (r == JL_OK) {
+            (*env)->SetLongArrayRegion(env, off, 0, (jsize)got, (const jlong *)o);
+            (*env)->SetIntArrayRegion(env, size, 0, (jsize)got, (const jint *)s);
+            (*env)->SetByteArrayRegion(env, kind, 0, (jsize)got, (const jbyte *)k);
+        }
+    }
+    free(k);
+    free(s);
+    free(o);
     return (r == JL_OK || r == JL_ERR_CAPACITY) ? (jlong)got : (jlong)r;
 }
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """C3 (1M mixed Zipf blocks, 1 B-64 KiB, one arena) through the general path,
-LAUNCHES times: a short driver for rocprofv3 PMC passes (JL_GENERAL picks the
-kernel: stream / gv4)."""
+LAUNCHES times: a short driver for rocprofv3 PMC passes (C3_PATH picks the
+kernel: auto / stream / gv4, through jl_set_option)."""
 import os
 import sys
 
@@ -14,6 +14,8 @@ import jleveldb_amd as jl  # noqa: E402
 SEED = 0x4A4C4442
 torch.cuda.set_device(0)
 jl.init(0)
+jl.set_option(jl.OPT_GENERAL_PATH, {"auto": jl.PATH_AUTO, "stream": jl.PATH_STREAM,
+                                    "gv4": jl.PATH_GV4}[os.environ.get("C3_PATH", "auto")])
 dev = torch.device("cuda:0")
 rng = np.random.default_rng(SEED)
 n = int(os.environ.get("C3_N", 1 << 20))
@@ -54,7 +56,7 @@ for i in range(L):
     ev[i + 1].record()
 torch.cuda.synchronize()
 t = [ev[i].elapsed_time(ev[i + 1]) for i in range(L)]
-print(os.environ.get("JL_GENERAL", "default"), "C3 bytes", int(lens.sum(dtype=np.uint64)), "ms", [round(x, 3) for x in t])
+print(os.environ.get("C3_PATH", "auto"), "C3 bytes", int(lens.sum(dtype=np.uint64)), "ms", [round(x, 3) for x in t])
 if os.environ.get("C3_STREAM"):  # read ceiling over the same arena
     sink = torch.zeros(1, dtype=torch.int32, device=dev)
     view = arena[: (total // 4096) * 4096]

@@ -24,7 +24,7 @@ TCC_EA0_RDREQ_sum
 GRBM_GUI_ACTIVE SQ_WAVES SQ_BUSY_CYCLES
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD
 SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM" TAG=${TAG} step pmc 600 bash tools/gpu_pmc.sh;;
-    tune) step tune 300 env VARIANTS="${VARIANTS:-1,2,3 1,2,7 1,2,8}" python tools/tune_fixed.py;;
+    tune) echo "tune: removed in r2 (study builds: tools/build_study.sh)";;
   esac
 done
 echo DONE
