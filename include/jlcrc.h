@@ -13,6 +13,14 @@
  *   - "_dev" functions take device pointers (HBM) and a hipStream_t (void*;
  *     NULL = the HIP null stream) and are asynchronous unless noted;
  *     the other batch functions take host memory and block until done;
+ *   - thread-safe: every calling thread gets its own streams, pinned staging
+ *     and device scratch (created on its first call, freed when it exits), so
+ *     concurrent callers do not serialise; jl_init / jl_shutdown must not race
+ *     with other calls;
+ *   - host-memory inputs stream through a double-buffered pipeline in chunks of
+ *     JL_STREAM_CHUNK_BYTES (the copy of chunk i+1 overlaps the kernels of
+ *     chunk i); pinned input is DMA'd directly, large pageable input is pinned
+ *     for the call (JL_OPT_HOST_REGISTER) or copied through pinned staging;
  *   - there is no CPU fallback behind the batch / verify entry points: with no
  *     usable GPU they fail with JL_ERR_NO_DEVICE.  Only the scalar Crc32C
  *     statics (first block) run on the host, as the reference's do.
@@ -80,11 +88,18 @@ const char *jl_version(void);
  *                            0 = equal block counts
  *   JL_OPT_SPLIT_CAP         crc batches: chunks available to split blocks above
  *                            512 KiB (-1 = min(2^20, 2048 n), the default)
+ *   JL_OPT_HOST_REGISTER     host-memory entry points: 1 = pin a pageable input of
+ *                            >= 64 MiB with hipHostRegister for the call and DMA it
+ *                            directly (the default), 0 = copy pageable input
+ *                            through pinned staging buffers
+ *   JL_OPT_STAGE_THREADS     host threads copying pageable input into staging (8)
  * Study builds only (make STUDY=1): JL_OPT_FIXED_KERNEL, JL_OPT_GV4_VARIANT. */
 #define JL_OPT_GENERAL_PATH 1
 #define JL_OPT_STREAM_DEPTH 2
 #define JL_OPT_STREAM_PARTITION 3
 #define JL_OPT_SPLIT_CAP 4
+#define JL_OPT_HOST_REGISTER 5
+#define JL_OPT_STAGE_THREADS 6
 #define JL_OPT_FIXED_KERNEL 100
 #define JL_OPT_GV4_VARIANT 101
 #define JL_PATH_AUTO 0

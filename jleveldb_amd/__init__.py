@@ -120,6 +120,17 @@ def _host(data) -> np.ndarray:
     return np.frombuffer(bytes(data), dtype=np.uint8)
 
 
+def _host_bytes(data):
+    """(pointer, size, keep-alive) of host input: a numpy array, bytes, or a
+    contiguous CPU torch tensor (pinned ones are DMA'd without staging)."""
+    if hasattr(data, "data_ptr"):
+        if data.is_cuda or not data.is_contiguous():
+            raise JLError("host entry point needs a contiguous CPU tensor")
+        return data.data_ptr(), data.numel() * data.element_size(), data
+    a = _host(data)
+    return a.ctypes.data, a.size, a
+
+
 # --------------------------------------------------------------------------
 # Crc32C mirror (J/util/Crc32C.java)
 # --------------------------------------------------------------------------
@@ -197,6 +208,7 @@ def shutdown() -> None:
 
 
 OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 3, 4
+OPT_HOST_REGISTER, OPT_STAGE_THREADS = 5, 6
 OPT_FIXED_KERNEL, OPT_GV4_VARIANT = 100, 101  # study builds only
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
 
@@ -251,11 +263,7 @@ def crc32c_fixed_dev(data, block_bytes: int, n_blocks: int | None = None, flags:
 def crc32c_fixed(data, block_bytes: int, n_blocks: int | None = None, flags: int = FLAG_MASK) -> np.ndarray:
     """Host-memory blocks (numpy array, bytes, or a pinned CPU tensor), streamed
     through the engine with overlapped H2D copies (jl_crc32c_fixed)."""
-    if hasattr(data, "data_ptr"):  # torch CPU tensor (pinned or not)
-        ptr, nbytes = data.data_ptr(), data.numel() * data.element_size()
-    else:
-        a = _host(data)
-        ptr, nbytes = a.ctypes.data, a.size
+    ptr, nbytes, _keep = _host_bytes(data)
     if n_blocks is None:
         n_blocks = nbytes // block_bytes
     if n_blocks * block_bytes > nbytes:
@@ -279,14 +287,15 @@ def crc32c_batch_dev(base, off, length, init=None, suffix=None, flags: int = FLA
 
 
 def crc32c_batch(base, off, length, init=None, suffix=None, flags: int = FLAG_MASK) -> np.ndarray:
-    """Host-memory batch (numpy): stages to the device, returns uint32 results."""
-    b = _host(base)
+    """Host-memory batch (numpy / bytes / CPU tensor arena): streamed to the
+    device in chunks (jl_crc32c_batch), returns uint32 results."""
+    b_ptr, b_size, _keep = _host_bytes(base)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     length = np.ascontiguousarray(length, dtype=np.uint32)
     init_a = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
     sfx_a = None if suffix is None else np.ascontiguousarray(suffix, dtype=np.uint8)
     out = np.zeros(off.size, dtype=np.uint32)
-    _check(lib().jl_crc32c_batch(b.ctypes.data, b.size, off.ctypes.data, length.ctypes.data,
+    _check(lib().jl_crc32c_batch(b_ptr, b_size, off.ctypes.data, length.ctypes.data,
                                  None if init_a is None else init_a.ctypes.data,
                                  None if sfx_a is None else sfx_a.ctypes.data, off.size, flags, out.ctypes.data),
            "jl_crc32c_batch")
@@ -295,11 +304,11 @@ def crc32c_batch(base, off, length, init=None, suffix=None, flags: int = FLAG_MA
 
 def table_verify(file, off, size) -> np.ndarray:
     """Batched TableFormat.readBlock checksum test over a host file image (1 = ok)."""
-    f = _host(file)
+    f_ptr, f_size, _keep = _host_bytes(file)
     off = np.ascontiguousarray(off, dtype=np.uint64)
     size = np.ascontiguousarray(size, dtype=np.uint32)
     st = np.zeros(off.size, dtype=np.uint8)
-    _check(lib().jl_table_verify(f.ctypes.data, f.size, off.ctypes.data, size.ctypes.data, off.size, st.ctypes.data),
+    _check(lib().jl_table_verify(f_ptr, f_size, off.ctypes.data, size.ctypes.data, off.size, st.ctypes.data),
            "jl_table_verify")
     return st
 
@@ -409,12 +418,13 @@ def log_emit_dev(src, plan, out=None, stream=None):
 
 
 def log_verify(log, checksum: bool = True) -> np.ndarray:
-    """Device verification of a host log image -> physical-record events (LOG_EVENT_DTYPE)."""
-    a = _host(log)
-    cap = a.size // 7 + 2
+    """Device verification of a host log image (numpy / bytes / CPU tensor) ->
+    physical-record events (LOG_EVENT_DTYPE).  `checksum`: bool or a LOG_* mode."""
+    ptr, size, _keep = _host_bytes(log)
+    cap = size // 7 + 2
     ev = np.zeros(cap, dtype=LOG_EVENT_DTYPE)
     n = ctypes.c_uint64(0)
-    _check(lib().jl_log_verify(a.ctypes.data if a.size else None, a.size, int(checksum), ev.ctypes.data, cap,
+    _check(lib().jl_log_verify(ptr if size else None, size, int(checksum), ev.ctypes.data, cap,
                                ctypes.byref(n)), "jl_log_verify")
     return ev[: n.value]
 

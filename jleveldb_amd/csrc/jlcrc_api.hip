@@ -8,6 +8,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/jlcrc.h"
@@ -63,35 +64,121 @@ struct DevBuf {
     }
 };
 
+// Grow-only pinned host buffer.
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// One half of a double-buffered host -> device pipeline: the device chunk and
+// its descriptors, pinned staging for pageable sources, a copy stream and two
+// events.  `copied`: the slot's H2D copies have landed; `used`: the compute and
+// copy-out that read the slot are done (the next copy into it waits for that).
+struct Slot {
+    DevBuf d_in, d_desc, d_out;  // chunk bytes, packed descriptor arrays, results
+    void *part[4] = {nullptr, nullptr, nullptr, nullptr};  // the descriptor arrays inside d_desc
+    PinBuf h_data, h_desc;
+    hipStream_t st = nullptr;
+    hipEvent_t copied = nullptr, used = nullptr;
+};
+
+// Per-thread workspace of the entry points that stage host memory or keep
+// scratch between launches (log verification).  Every calling thread has its
+// own streams, staging and scratch, so concurrent callers neither share
+// buffers nor serialise on a lock (r1 had one process-wide mutex).  Created on
+// a thread's first call; released when the thread exits or by jl_shutdown.
+struct Workspace {
+    hipStream_t stream = nullptr;  // compute stream of the host-memory entry points
+    DevBuf ws_cnt, ws_start, ws_slot, ws_off, ws_len, ws_ok, ws_tmp;  // two-pass log verify
+    DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
+    Slot slot[2];
+    void release() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (DevBuf *b : {&ws_cnt, &ws_start, &ws_slot, &ws_off, &ws_len, &ws_ok, &ws_tmp, &ws_ls, &ws_lsev})
+            b->release();
+        for (Slot &sl : slot) {
+            if (sl.st) (void)hipStreamSynchronize(sl.st);
+            for (DevBuf *b : {&sl.d_in, &sl.d_desc, &sl.d_out}) b->release();
+            sl.h_data.release();
+            sl.h_desc.release();
+            if (sl.copied) (void)hipEventDestroy(sl.copied);
+            if (sl.used) (void)hipEventDestroy(sl.used);
+            if (sl.st) (void)hipStreamDestroy(sl.st);
+            sl = Slot();
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+};
+
 struct Context {
-    std::mutex mu;  // guards init and the staging workspace of the host-memory entry points
+    std::mutex mu;  // guards init / shutdown and the workspace registry
     bool ready = false;
     int device = -1;
+    int gen = 0;  // bumped by every jl_init: threads re-bind their HIP device
     int cus = 0;
-    hipStream_t stream = nullptr;
     void *d_img = nullptr;   // 160 KiB LDS image
     void *d_img_v4[4] = {nullptr, nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block; [3] gv4
     void *d_img_log = nullptr;  // fused log-verify image (log_stream.hip)
     uint32_t *d_aux = nullptr;
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
     uint32_t *d_scratch = nullptr;  // 4 KiB sink for stores of out-of-range pair members
-    // staging workspace (host-memory APIs, log verify)
-    DevBuf ws_data, ws_off, ws_len, ws_init, ws_sfx, ws_out, ws_cnt, ws_start, ws_ev, ws_ok, ws_tmp, ws_slot;
-    DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
-    // streaming pipeline (jl_crc32c_fixed): two slots, each a device chunk + result
-    // buffer, a pinned staging buffer (pageable sources) and its own stream
-    struct Slot {
-        DevBuf d_in, d_out;
-        void *h_stage = nullptr;
-        size_t h_cap = 0;
-        hipStream_t st = nullptr;
-        hipEvent_t done = nullptr;
-    } slot[2];
+    std::vector<Workspace *> live;  // every thread's workspace (jl_shutdown releases them)
 };
 
 Context &ctx() {
     static Context c;
     return c;
+}
+
+// Owner of the calling thread's workspace: releases it when the thread exits.
+struct WsOwner {
+    Workspace *w = nullptr;
+    ~WsOwner() {
+        if (!w) return;
+        Context &c = ctx();
+        std::lock_guard<std::mutex> lk(c.mu);
+        c.live.erase(std::remove(c.live.begin(), c.live.end(), w), c.live.end());
+        if (c.ready && hipSetDevice(c.device) == hipSuccess) w->release();
+        delete w;
+    }
+};
+thread_local WsOwner t_ws;
+thread_local int t_gen = -1;  // the context generation this thread's HIP device is bound for
+
+// The calling thread's workspace with its streams and events created.
+int get_ws(Workspace **out) {
+    if (!t_ws.w) {
+        Workspace *w = new Workspace;
+        Context &c = ctx();
+        std::lock_guard<std::mutex> lk(c.mu);
+        c.live.push_back(w);
+        t_ws.w = w;
+    }
+    Workspace &w = *t_ws.w;
+    if (!w.stream) JL_HIP(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    for (Slot &sl : w.slot) {
+        if (!sl.st) JL_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+        if (!sl.copied) JL_HIP(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+        if (!sl.used) JL_HIP(hipEventCreateWithFlags(&sl.used, hipEventDisableTiming));
+    }
+    *out = &w;
+    return JL_OK;
 }
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
@@ -102,6 +189,8 @@ struct Options {
     int stream_depth = 16;            // JL_OPT_STREAM_DEPTH: 16 / 32 / 48 ring entries
     int partition = 1;                // JL_OPT_STREAM_PARTITION: byte-balanced wave ranges
     int64_t split_cap = -1;           // JL_OPT_SPLIT_CAP: chunks of split blocks (-1: min(2^20, 2048 n))
+    int host_register = 1;            // JL_OPT_HOST_REGISTER: pin pageable inputs >= 64 MiB for the call
+    int stage_threads = 8;            // JL_OPT_STAGE_THREADS: host threads copying into pinned staging
     int fixed_kernel = 7;             // study: JL_OPT_FIXED_KERNEL (7 = the v4 product kernel)
     int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
 };
@@ -110,11 +199,209 @@ Options &opt() {
     return o;
 }
 
+// Initialises the engine on device 0 if no jl_init came first, and binds the
+// calling thread to the engine's device (HIP's current device is per thread).
 int ensure_ready() {
     Context &c = ctx();
-    if (c.ready) return JL_OK;
-    int r = jl_init(0);
-    return r;
+    if (!c.ready)
+        if (int r = jl_init(0)) return r;
+    if (t_gen != c.gen) {
+        JL_HIP(hipSetDevice(c.device));
+        t_gen = c.gen;
+    }
+    return JL_OK;
+}
+
+// ------------------------------------------------------- host input staging
+constexpr uint64_t kRegisterMin = 64ull << 20;  // hipHostRegister only pays for large inputs
+
+// A host input range for one call: DMA'd directly when it is pinned
+// (hipHostMalloc'ed or already registered) or could be registered for the call
+// (JL_OPT_HOST_REGISTER), else copied through the slots' pinned staging.
+struct HostSrc {
+    const uint8_t *p = nullptr;
+    bool direct = false, registered = false;
+    HostSrc(const void *ptr, uint64_t bytes) : p((const uint8_t *)ptr) {
+        hipPointerAttribute_t attr;
+        direct = hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeHost;
+        (void)hipGetLastError();  // pageable memory reports an error here; clear it
+        if (!direct && opt().host_register && bytes >= kRegisterMin) {
+            // read-only first: an mmap'd file opened O_RDONLY can only be pinned that way
+            for (unsigned flags : {(unsigned)hipHostRegisterReadOnly, (unsigned)hipHostRegisterDefault}) {
+                if (hipHostRegister((void *)ptr, bytes, flags) == hipSuccess) {
+                    direct = registered = true;
+                    break;
+                }
+                (void)hipGetLastError();  // not registrable (e.g. some file mappings): staging
+            }
+        }
+    }
+    ~HostSrc() {
+        if (registered) (void)hipHostUnregister((void *)p);
+    }
+};
+
+// memcpy split over up to JL_OPT_STAGE_THREADS threads (pageable -> pinned
+// staging runs at one core's copy rate otherwise, well under PCIe's)
+void par_memcpy(void *dst, const void *src, size_t n) {
+    const size_t piece = 4ull << 20;
+    const int t = (int)std::min<size_t>((size_t)std::max(1, opt().stage_threads), n / piece);
+    if (t <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = ((n + t - 1) / t + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int i = 1; i < t && (size_t)i * per < n; i++) {
+        const size_t a = (size_t)i * per, b = std::min(n, a + per);
+        th.emplace_back([=] { memcpy((char *)dst + a, (const char *)src + a, b - a); });
+    }
+    memcpy(dst, src, std::min(n, per));
+    for (auto &x : th) x.join();
+}
+
+// Enqueues the copy of src.p[off, off + bytes) into sl.d_in on the slot's copy
+// stream, after the slot's previous use; staged through pinned memory when the
+// source is pageable.
+int slot_put_data(Slot &sl, const HostSrc &src, uint64_t off, uint64_t bytes) {
+    JL_HIP(hipStreamWaitEvent(sl.st, sl.used, 0));
+    const uint8_t *p = src.p + off;
+    if (!src.direct) {
+        JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
+        JL_HIP(sl.h_data.ensure(bytes));
+        par_memcpy(sl.h_data.p, p, bytes);
+        p = (const uint8_t *)sl.h_data.p;
+    }
+    if (bytes) JL_HIP(hipMemcpyAsync(sl.d_in.p, p, bytes, hipMemcpyHostToDevice, sl.st));
+    return JL_OK;
+}
+
+// Enqueues the copy of a chunk's descriptor arrays (host arrays, null ones
+// skipped) packed into sl.d_desc through the slot's pinned descriptor staging
+// (256-B aligned parts, one H2D copy); sl.part[k] = the device address of part
+// k (null for a null source).
+struct Part {
+    const void *src;
+    size_t bytes;
+};
+constexpr size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+int slot_put_desc(Slot &sl, std::initializer_list<Part> parts) {
+    void **dev = sl.part;
+    size_t total = 0;
+    for (const Part &p : parts) total += p.src ? align256(p.bytes) : 0;
+    JL_HIP(hipStreamWaitEvent(sl.st, sl.used, 0));
+    JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
+    JL_HIP(sl.h_desc.ensure(total));
+    JL_HIP(sl.d_desc.ensure(total));
+    size_t at = 0;
+    int k = 0;
+    for (const Part &p : parts) {
+        dev[k++] = p.src ? (char *)sl.d_desc.p + at : nullptr;
+        if (!p.src) continue;
+        memcpy((char *)sl.h_desc.p + at, p.src, p.bytes);
+        at += align256(p.bytes);
+    }
+    if (total) JL_HIP(hipMemcpyAsync(sl.d_desc.p, sl.h_desc.p, total, hipMemcpyHostToDevice, sl.st));
+    return JL_OK;
+}
+
+// Waits for both pipelines' work to finish and returns the first error of the
+// call, if any.
+int drain(Workspace &w, int rc) {
+    hipError_t e = hipStreamSynchronize(w.stream);
+    for (Slot &sl : w.slot) {
+        hipError_t f = hipStreamSynchronize(sl.st);
+        if (e == hipSuccess) e = f;
+    }
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(JL_ERR_HIP, std::string("pipeline: ") + hipGetErrorString(e));
+    return JL_OK;
+}
+
+// Double-buffered host -> device pipeline over n_chunks chunks.  put(i, slot)
+// enqueues chunk i's copies on the slot's copy stream; run(i, slot) enqueues
+// its kernels and copy-out on the compute stream.  Chunk i+1's copy is enqueued
+// before chunk i's compute, so the copy engine always has the next chunk queued
+// and a copy-out that blocks the host (pageable destination) never starves it.
+template <class Put, class Run>
+int pipeline(Workspace &w, uint64_t n_chunks, Put put, Run run) {
+    auto issue = [&](uint64_t i) -> int {
+        Slot &sl = w.slot[i & 1];
+        if (int r = put(i, sl)) return r;
+        JL_HIP(hipEventRecord(sl.copied, sl.st));
+        return JL_OK;
+    };
+    int rc = n_chunks ? issue(0) : JL_OK;
+    for (uint64_t i = 0; i < n_chunks && !rc; i++) {
+        if (i + 1 < n_chunks && (rc = issue(i + 1))) break;
+        Slot &sl = w.slot[i & 1];
+        hipError_t e = hipStreamWaitEvent(w.stream, sl.copied, 0);
+        if (e != hipSuccess) {
+            rc = fail(JL_ERR_HIP, std::string("pipeline: ") + hipGetErrorString(e));
+            break;
+        }
+        if ((rc = run(i, sl))) break;
+        e = hipEventRecord(sl.used, w.stream);
+        if (e != hipSuccess) rc = fail(JL_ERR_HIP, std::string("pipeline: ") + hipGetErrorString(e));
+    }
+    return drain(w, rc);
+}
+
+constexpr uint64_t kSlack = 256;                // device bytes past a chunk (rounded-up tail reads)
+constexpr uint64_t kChunkBlocks = 1ull << 20;   // descriptors per chunk
+
+// Chunks of an offset/length batch: blocks [a, b) whose bytes (with `extra`
+// trailing bytes each) lie in the host window [lo, hi).
+struct Chunk {
+    uint64_t a, b, lo, hi;
+};
+// When the offsets ascend (a table's handles, an arena of appended blocks) the
+// blocks are cut into chunks whose windows span at most JL_STREAM_CHUNK_BYTES
+// (a larger block is a chunk of its own); otherwise one chunk spans them all.
+// Window starts are page-aligned (DMA).  Blocks were range-checked by the caller.
+std::vector<Chunk> plan_chunks(const uint64_t *off, const uint32_t *len, uint32_t extra, uint64_t n) {
+    std::vector<Chunk> ch;
+    bool asc = true;
+    for (uint64_t i = 1; i < n && asc; i++) asc = off[i] >= off[i - 1];
+    auto page = [](uint64_t x) { return x & ~4095ull; };
+    if (!asc) {
+        uint64_t lo = ~0ull, hi = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            lo = std::min(lo, off[i]);
+            hi = std::max(hi, off[i] + len[i] + extra);
+        }
+        ch.push_back({0, n, page(lo), hi});
+        return ch;
+    }
+    for (uint64_t a = 0; a < n;) {
+        const uint64_t lo = page(off[a]);
+        uint64_t hi = off[a] + len[a] + extra, b = a + 1;
+        while (b < n && b - a < kChunkBlocks) {
+            const uint64_t h = std::max(hi, off[b] + len[b] + extra);
+            if (h - lo > JL_STREAM_CHUNK_BYTES) break;
+            hi = h;
+            b++;
+        }
+        ch.push_back({a, b, lo, hi});
+        a = b;
+    }
+    return ch;
+}
+
+// Sizes both slots for the largest chunk: window bytes, results of out_bytes and
+// descriptors of desc_bytes a block.
+int ensure_chunk_bufs(Workspace &w, const std::vector<Chunk> &ch, size_t out_bytes, size_t desc_bytes) {
+    uint64_t win = 0, m = 0;
+    for (const Chunk &k : ch) {
+        win = std::max(win, k.hi - k.lo);
+        m = std::max(m, k.b - k.a);
+    }
+    for (Slot &sl : w.slot) {
+        JL_HIP(sl.d_in.ensure(win + kSlack));
+        JL_HIP(sl.d_out.ensure(m * out_bytes));
+        JL_HIP(sl.d_desc.ensure(m * desc_bytes + 4 * 256));
+    }
+    return JL_OK;
 }
 
 // NULL is HIP's null (legacy default) stream, as everywhere in HIP, so device
@@ -388,6 +675,14 @@ int jl_set_option(int option, int64_t value) {
         if (value < -1 || value > 0x7fffffff) break;
         o.split_cap = value;
         return JL_OK;
+    case JL_OPT_HOST_REGISTER:
+        if (value != 0 && value != 1) break;
+        o.host_register = (int)value;
+        return JL_OK;
+    case JL_OPT_STAGE_THREADS:
+        if (value < 1 || value > 64) break;
+        o.stage_threads = (int)value;
+        return JL_OK;
 #if JL_STUDY
     case JL_OPT_FIXED_KERNEL:
         o.fixed_kernel = (int)value;
@@ -410,6 +705,8 @@ int64_t jl_get_option(int option) {
     case JL_OPT_STREAM_DEPTH: return o.stream_depth;
     case JL_OPT_STREAM_PARTITION: return o.partition;
     case JL_OPT_SPLIT_CAP: return o.split_cap;
+    case JL_OPT_HOST_REGISTER: return o.host_register;
+    case JL_OPT_STAGE_THREADS: return o.stage_threads;
     case JL_OPT_FIXED_KERNEL: return o.fixed_kernel;
     case JL_OPT_GV4_VARIANT: return o.gv4_variant;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
@@ -446,7 +743,6 @@ int jl_init(int device) {
         }
         (void)hipGetLastError();
     }
-    JL_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     std::vector<uint32_t> img = jlmath::build_lds_image();
     std::vector<uint32_t> aux = jlmath::build_aux();
     JL_HIP(hipMalloc(&c.d_img, jlmath::kImageBytes));
@@ -467,6 +763,8 @@ int jl_init(int device) {
     JL_HIP(hipMemcpy(c.d_aux, aux.data(), aux.size() * 4, hipMemcpyHostToDevice));
     JL_HIP(hipMemset(c.d_zero, 0, 4096));
     c.device = device;
+    c.gen++;
+    t_gen = c.gen;
     c.ready = true;
     return JL_OK;
 }
@@ -476,18 +774,8 @@ int jl_shutdown(void) {
     std::lock_guard<std::mutex> lk(c.mu);
     if (!c.ready) return JL_OK;
     (void)hipSetDevice(c.device);
-    (void)hipStreamSynchronize(c.stream);
-    for (DevBuf *b : {&c.ws_data, &c.ws_off, &c.ws_len, &c.ws_init, &c.ws_sfx, &c.ws_out, &c.ws_cnt, &c.ws_start,
-                      &c.ws_ev, &c.ws_ok, &c.ws_tmp, &c.ws_slot, &c.ws_ls, &c.ws_lsev})
-        b->release();
-    for (auto &sl : c.slot) {
-        sl.d_in.release();
-        sl.d_out.release();
-        if (sl.h_stage) (void)hipHostFree(sl.h_stage);
-        if (sl.done) (void)hipEventDestroy(sl.done);
-        if (sl.st) (void)hipStreamDestroy(sl.st);
-        sl = Context::Slot();
-    }
+    (void)hipDeviceSynchronize();
+    for (Workspace *w : c.live) w->release();  // their threads recreate them after the next jl_init
     (void)hipFree(c.d_img);
     (void)hipFree(c.d_img_log);
     c.d_img_log = nullptr;
@@ -499,11 +787,9 @@ int jl_shutdown(void) {
     (void)hipFree(c.d_zero);
     (void)hipFree(c.d_scratch);
     c.d_scratch = nullptr;
-    (void)hipStreamDestroy(c.stream);
     c.d_img = nullptr;
     c.d_aux = nullptr;
     c.d_zero = nullptr;
-    c.stream = nullptr;
     c.ready = false;
     c.device = -1;
     return JL_OK;
@@ -551,44 +837,28 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     if (n_blocks == 0) return JL_OK;
     if (!host || !out || block_bytes == 0) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: bad arguments");
     if (block_bytes > JL_STREAM_CHUNK_BYTES) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: block larger than a chunk");
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
-    hipPointerAttribute_t attr;
-    bool pinned = hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost;
-    (void)hipGetLastError();  // pageable memory reports an error here; clear it
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
     const uint64_t per = JL_STREAM_CHUNK_BYTES / block_bytes;  // blocks per chunk
-    const uint64_t chunk_bytes = per * block_bytes;
-    for (auto &sl : c.slot) {
-        if (!sl.st) JL_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
-        if (!sl.done) JL_HIP(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-        JL_HIP(sl.d_in.ensure(chunk_bytes));
-        JL_HIP(sl.d_out.ensure(per * 4));
-        if (!pinned && sl.h_cap < chunk_bytes) {
-            if (sl.h_stage) (void)hipHostFree(sl.h_stage);
-            sl.h_stage = nullptr;
-            sl.h_cap = 0;
-            if (hipHostMalloc(&sl.h_stage, chunk_bytes, hipHostMallocDefault) != hipSuccess)
-                return fail(JL_ERR_NOMEM, "jl_crc32c_fixed: pinned staging allocation failed");
-            sl.h_cap = chunk_bytes;
-        }
+    const uint64_t first = std::min(per, n_blocks);
+    for (Slot &sl : w->slot) {
+        JL_HIP(sl.d_in.ensure(first * block_bytes + kSlack));
+        JL_HIP(sl.d_out.ensure(first * 4));
     }
-    for (uint64_t b0 = 0, i = 0; b0 < n_blocks; b0 += per, i++) {
-        Context::Slot &sl = c.slot[i & 1];
-        const uint64_t nb = std::min(per, n_blocks - b0);
-        const uint8_t *src = host + b0 * block_bytes;
-        if (!pinned) {  // the slot's previous copy out of its staging buffer must be done
-            JL_HIP(hipEventSynchronize(sl.done));
-            memcpy(sl.h_stage, src, nb * block_bytes);
-            src = (const uint8_t *)sl.h_stage;
-        }
-        JL_HIP(hipMemcpyAsync(sl.d_in.p, src, nb * block_bytes, hipMemcpyHostToDevice, sl.st));
-        if (int r = jl_crc32c_fixed_dev(sl.d_in.p, block_bytes, nb, flags, (uint32_t *)sl.d_out.p, sl.st)) return r;
-        JL_HIP(hipMemcpyAsync(out + b0, sl.d_out.p, nb * 4, hipMemcpyDeviceToHost, sl.st));
-        JL_HIP(hipEventRecord(sl.done, sl.st));
-    }
-    JL_HIP(hipStreamSynchronize(c.slot[0].st));
-    JL_HIP(hipStreamSynchronize(c.slot[1].st));
-    return JL_OK;
+    HostSrc src(host, n_blocks * block_bytes);
+    const uint64_t n_chunks = (n_blocks + per - 1) / per;
+    return pipeline(
+        *w, n_chunks,
+        [&](uint64_t i, Slot &sl) {
+            return slot_put_data(sl, src, i * per * block_bytes, std::min(per, n_blocks - i * per) * block_bytes);
+        },
+        [&](uint64_t i, Slot &sl) -> int {
+            const uint64_t b0 = i * per, nb = std::min(per, n_blocks - b0);
+            if (int r = jl_crc32c_fixed_dev(sl.d_in.p, block_bytes, nb, flags, (uint32_t *)sl.d_out.p, w->stream))
+                return r;
+            JL_HIP(hipMemcpyAsync(out + b0, sl.d_out.p, nb * 4, hipMemcpyDeviceToHost, w->stream));
+            return JL_OK;
+        });
 }
 
 int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t *d_off, const uint32_t *d_len,
@@ -615,35 +885,36 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
     if (!base || !off || !len || !out) return fail(JL_ERR_INVALID, "jl_crc32c_batch: null pointer");
     for (uint64_t i = 0; i < n; i++)
         if (off[i] + (uint64_t)len[i] > base_bytes) return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
-    hipStream_t st = c.stream;
-    JL_HIP(c.ws_data.ensure(base_bytes + 16));
-    JL_HIP(c.ws_off.ensure(n * 8));
-    JL_HIP(c.ws_len.ensure(n * 4));
-    JL_HIP(c.ws_out.ensure(n * 4));
-    JL_HIP(hipMemcpyAsync(c.ws_data.p, base, base_bytes, hipMemcpyHostToDevice, st));
-    JL_HIP(hipMemcpyAsync(c.ws_off.p, off, n * 8, hipMemcpyHostToDevice, st));
-    JL_HIP(hipMemcpyAsync(c.ws_len.p, len, n * 4, hipMemcpyHostToDevice, st));
-    jlk::KParams P = base_params(c.ws_data.p, n, jlk::MODE_CRC);
-    P.off = (const uint64_t *)c.ws_off.p;
-    P.len = (const uint32_t *)c.ws_len.p;
-    if (init) {
-        JL_HIP(c.ws_init.ensure(n * 4));
-        JL_HIP(hipMemcpyAsync(c.ws_init.p, init, n * 4, hipMemcpyHostToDevice, st));
-        P.init = (const uint32_t *)c.ws_init.p;
-    }
-    if (suffix) {
-        JL_HIP(c.ws_sfx.ensure(n));
-        JL_HIP(hipMemcpyAsync(c.ws_sfx.p, suffix, n, hipMemcpyHostToDevice, st));
-        P.suffix = (const uint8_t *)c.ws_sfx.p;
-    }
-    P.flags = flags;
-    P.out32 = (uint32_t *)c.ws_out.p;
-    if (int r = run_general(P, st)) return r;
-    JL_HIP(hipMemcpyAsync(out, c.ws_out.p, n * 4, hipMemcpyDeviceToHost, st));
-    JL_HIP(hipStreamSynchronize(st));
-    return JL_OK;
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    const std::vector<Chunk> ch = plan_chunks(off, len, 0, n);
+    if (int r = ensure_chunk_bufs(*w, ch, 4, 8 + 4 + 4 + 1)) return r;
+    HostSrc src(base, base_bytes);
+    return pipeline(
+        *w, ch.size(),
+        [&](uint64_t i, Slot &sl) -> int {
+            const Chunk &k = ch[i];
+            if (int r = slot_put_data(sl, src, k.lo, k.hi - k.lo)) return r;
+            const uint64_t m = k.b - k.a;
+            return slot_put_desc(sl, {{off + k.a, m * 8}, {len + k.a, m * 4}, {init ? init + k.a : nullptr, m * 4},
+                                      {suffix ? suffix + k.a : nullptr, m}});
+        },
+        [&](uint64_t i, Slot &sl) -> int {
+            const Chunk &k = ch[i];
+            const uint64_t m = k.b - k.a;
+            // the window [lo, hi) sits at d_in[0]: offsets stay arena offsets
+            jlk::KParams P = base_params((const uint8_t *)sl.d_in.p - k.lo, m, jlk::MODE_CRC);
+            P.base_bytes = k.hi;
+            P.off = (const uint64_t *)sl.part[0];
+            P.len = (const uint32_t *)sl.part[1];
+            P.init = (const uint32_t *)sl.part[2];
+            P.suffix = (const uint8_t *)sl.part[3];
+            P.flags = flags;
+            P.out32 = (uint32_t *)sl.d_out.p;
+            if (int r = run_general(P, w->stream)) return r;
+            JL_HIP(hipMemcpyAsync(out + k.a, sl.d_out.p, m * 4, hipMemcpyDeviceToHost, w->stream));
+            return JL_OK;
+        });
 }
 
 // ------------------------------------------------------------- table shims
@@ -682,25 +953,32 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
     for (uint64_t i = 0; i < n; i++)
         if (off[i] + (uint64_t)size[i] + 5 > file_bytes)
             return fail(JL_ERR_INVALID, "jl_table_verify: truncated block read");  // TableFormat.java:203-206
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
-    hipStream_t st = c.stream;
-    JL_HIP(c.ws_data.ensure(file_bytes + 16));
-    JL_HIP(c.ws_off.ensure(n * 8));
-    JL_HIP(c.ws_len.ensure(n * 4));
-    JL_HIP(c.ws_ok.ensure(n));
-    JL_HIP(hipMemcpyAsync(c.ws_data.p, file, file_bytes, hipMemcpyHostToDevice, st));
-    JL_HIP(hipMemcpyAsync(c.ws_off.p, off, n * 8, hipMemcpyHostToDevice, st));
-    JL_HIP(hipMemcpyAsync(c.ws_len.p, size, n * 4, hipMemcpyHostToDevice, st));
-    jlk::KParams P = base_params(c.ws_data.p, n, jlk::MODE_TABLE_VERIFY);
-    P.off = (const uint64_t *)c.ws_off.p;
-    P.len = (const uint32_t *)c.ws_len.p;
-    P.len_add = 1;
-    P.out8 = (uint8_t *)c.ws_ok.p;
-    if (int r = run_general(P, st)) return r;
-    JL_HIP(hipMemcpyAsync(status, c.ws_ok.p, n, hipMemcpyDeviceToHost, st));
-    JL_HIP(hipStreamSynchronize(st));
-    return JL_OK;
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    const std::vector<Chunk> ch = plan_chunks(off, size, 5, n);  // block || 5-byte trailer
+    if (int r = ensure_chunk_bufs(*w, ch, 1, 8 + 4)) return r;
+    HostSrc src(file, file_bytes);
+    return pipeline(
+        *w, ch.size(),
+        [&](uint64_t i, Slot &sl) -> int {
+            const Chunk &k = ch[i];
+            if (int r = slot_put_data(sl, src, k.lo, k.hi - k.lo)) return r;
+            const uint64_t m = k.b - k.a;
+            return slot_put_desc(sl, {{off + k.a, m * 8}, {size + k.a, m * 4}});
+        },
+        [&](uint64_t i, Slot &sl) -> int {
+            const Chunk &k = ch[i];
+            const uint64_t m = k.b - k.a;
+            jlk::KParams P = base_params((const uint8_t *)sl.d_in.p - k.lo, m, jlk::MODE_TABLE_VERIFY);
+            P.base_bytes = k.hi;
+            P.off = (const uint64_t *)sl.part[0];
+            P.len = (const uint32_t *)sl.part[1];
+            P.len_add = 1;  // block || type byte
+            P.out8 = (uint8_t *)sl.d_out.p;
+            if (int r = run_general(P, w->stream)) return r;
+            JL_HIP(hipMemcpyAsync(status + k.a, sl.d_out.p, m, hipMemcpyDeviceToHost, w->stream));
+            return JL_OK;
+        });
 }
 
 // --------------------------------------------------------------- log shims
@@ -725,25 +1003,24 @@ int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uin
     if (n_frags == 0 && log_bytes == 0) return JL_OK;
     if (!d_log || (n_frags && (!d_src || !d_frag_hdr_off || !d_frag_src_off || !d_frag_len || !d_frag_type)))
         return fail(JL_ERR_INVALID, "jl_log_emit_dev: null pointer");
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);  // ws_off holds the payload offsets
     hipStream_t st = pick(stream);
     JL_HIP(hipMemsetAsync(d_log, 0, log_bytes, st));  // block trailers (J/db/LogWriter.java:101-107)
     if (n_frags == 0) return JL_OK;
-    JL_HIP(c.ws_off.ensure(n_frags * 8));
-    uint64_t *pay = (uint64_t *)c.ws_off.p;
-    JL_HIP(jlk::launch_log_copy((const uint8_t *)d_src, d_frag_src_off, d_frag_hdr_off, d_frag_len, n_frags, d_log,
-                                pay, st));
+    uint64_t *pay = nullptr;  // payload offsets: stream-ordered scratch, so the call stays asynchronous
+    if (hipMallocAsync((void **)&pay, n_frags * 8, st) != hipSuccess)
+        return fail(JL_ERR_NOMEM, "jl_log_emit_dev: scratch allocation failed");
+    hipError_t e = jlk::launch_log_copy((const uint8_t *)d_src, d_frag_src_off, d_frag_hdr_off, d_frag_len, n_frags,
+                                        d_log, pay, st);
     jlk::KParams P = base_params(d_log, n_frags, jlk::MODE_LOG_HEADER);
     P.off = pay;
     P.len = d_frag_len;
     P.type = d_frag_type;
     P.out8 = d_log;
     P.hdr_off = d_frag_hdr_off;
-    if (int r = run_general(P, st)) return r;
-    // the workspace is reused by the next call: finish before releasing the lock
-    JL_HIP(hipStreamSynchronize(st));
-    return JL_OK;
+    const int r = e == hipSuccess ? run_general(P, st) : JL_OK;
+    (void)hipFreeAsync(pay, st);
+    JL_HIP(e);
+    return r;
 }
 
 // Fused path (log_stream.hip): one streaming kernel walks and verifies every
@@ -753,9 +1030,8 @@ int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uin
 // per-block slots: *fallback is set and nothing is written.
 constexpr uint32_t kLogStreamCap = 256;
 
-static int log_verify_stream(const void *d_log, uint64_t log_bytes, jl_log_event *d_events, uint64_t cap,
-                             uint64_t *n_events, hipStream_t st, bool *fallback) {
-    Context &c = ctx();
+static int log_verify_stream(Workspace &c, const void *d_log, uint64_t log_bytes, jl_log_event *d_events,
+                             uint64_t cap, uint64_t *n_events, hipStream_t st, bool *fallback) {
     *fallback = false;
     const uint64_t nb = (log_bytes + 32767) / 32768;
     if (nb >= (1ull << 31)) {
@@ -780,7 +1056,7 @@ static int log_verify_stream(const void *d_log, uint64_t log_bytes, jl_log_event
     uint64_t *start = (uint64_t *)(ws + st_off);
     JL_HIP(hipMemsetAsync(A.count + nb, 0, 4, st));  // count[nb] = 0: start[nb] is the total
     JL_HIP(hipMemsetAsync(A.overflow, 0, 4, st));
-    JL_HIP(jlk::launch_logstream(c.d_img_log, A, c.cus, st));
+    JL_HIP(jlk::launch_logstream(ctx().d_img_log, A, ctx().cus, st));
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
     size_t tmp = 0;
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, it, start, (int)(nb + 1), st));
@@ -801,14 +1077,17 @@ static int log_verify_stream(const void *d_log, uint64_t log_bytes, jl_log_event
     return JL_OK;
 }
 
-static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
-                           uint64_t *n_events, hipStream_t st) {
-    Context &c = ctx();
+// Verifies d_log[0, log_bytes) on `st` with the calling thread's scratch `c`.
+// *n_events is known on return (the event count is read back); with sync_end
+// the events are complete too, else they complete in stream order (the host
+// pipeline copies them out on the same stream).
+static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events,
+                           uint64_t cap, uint64_t *n_events, hipStream_t st, bool sync_end) {
     if (checksum == JL_LOG_CHECKSUM_FUSED) {  // the single-pass kernel, unless a block overflows its slots
         bool fallback = false;
         *n_events = 0;
         if (log_bytes == 0) return JL_OK;
-        if (int r = log_verify_stream(d_log, log_bytes, d_events, cap, n_events, st, &fallback)) return r;
+        if (int r = log_verify_stream(c, d_log, log_bytes, d_events, cap, n_events, st, &fallback)) return r;
         if (!fallback) return JL_OK;
     }
     const uint64_t nb = (log_bytes + 32767) / 32768;
@@ -847,7 +1126,7 @@ static int log_verify_impl(const void *d_log, uint64_t log_bytes, int checksum, 
         JL_HIP(jlk::launch_log_finalize(nb, start, cnt, (const uint8_t *)c.ws_ok.p, (jlk::LogEvent *)d_events, 1, total,
                                         (unsigned long long *)c.ws_slot.p, st));
     }
-    JL_HIP(hipStreamSynchronize(st));
+    if (sync_end) JL_HIP(hipStreamSynchronize(st));
     return JL_OK;
 }
 
@@ -856,35 +1135,52 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
     if (int r = ensure_ready()) return r;
     if (!n_events || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev: null pointer");
     if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify_dev: bad checksum mode");
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);  // shares the walk workspace
-    return log_verify_impl(d_log, log_bytes, checksum, d_events, cap, n_events, pick(stream));
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    return log_verify_impl(*w, d_log, log_bytes, checksum, d_events, cap, n_events, pick(stream), true);
 }
 
+// Host-memory log verification: chunks of JL_STREAM_CHUNK_BYTES (whole 32 KiB
+// blocks, so no record straddles a chunk and the final short block is the last
+// chunk's) through the double-buffered pipeline; each chunk's events are moved
+// to file offsets and copied out while the next chunk's bytes are in flight.
 int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_event *events, uint64_t cap,
                   uint64_t *n_events) {
     if (int r = ensure_ready()) return r;
     if (!n_events || (log_bytes && !log)) return fail(JL_ERR_INVALID, "jl_log_verify: null pointer");
     if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify: bad checksum mode");
-    Context &c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
-    hipStream_t st = c.stream;
+    static_assert(JL_STREAM_CHUNK_BYTES % 32768 == 0, "log chunks must be whole blocks");
     *n_events = 0;
     if (log_bytes == 0) return JL_OK;
-    JL_HIP(c.ws_data.ensure(log_bytes + 16));
-    JL_HIP(hipMemcpyAsync(c.ws_data.p, log, log_bytes, hipMemcpyHostToDevice, st));
-    // events land in ws_ev, then copy out
-    const uint64_t ev_cap = log_bytes / 7 + 2;  // upper bound on physical records
-    JL_HIP(c.ws_ev.ensure(ev_cap * sizeof(jl_log_event)));
-    uint64_t total = 0;
-    int r = log_verify_impl(c.ws_data.p, log_bytes, checksum, (jl_log_event *)c.ws_ev.p, ev_cap, &total, st);
-    *n_events = total;
-    if (r) return r;
-    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
-    if (total) {
-        JL_HIP(hipMemcpyAsync(events, c.ws_ev.p, total * sizeof(jl_log_event), hipMemcpyDeviceToHost, st));
-        JL_HIP(hipStreamSynchronize(st));
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    const uint64_t CH = JL_STREAM_CHUNK_BYTES, first = std::min(CH, log_bytes);
+    const uint64_t ev_cap = first / 7 + 2;  // upper bound on a chunk's physical records
+    for (Slot &sl : w->slot) {
+        JL_HIP(sl.d_in.ensure(first + kSlack));
+        JL_HIP(sl.d_out.ensure(ev_cap * sizeof(jl_log_event)));
     }
+    HostSrc src(log, log_bytes);
+    uint64_t total = 0;
+    const int rc = pipeline(
+        *w, (log_bytes + CH - 1) / CH,
+        [&](uint64_t i, Slot &sl) { return slot_put_data(sl, src, i * CH, std::min(CH, log_bytes - i * CH)); },
+        [&](uint64_t i, Slot &sl) -> int {
+            uint64_t n = 0;
+            jl_log_event *ev = (jl_log_event *)sl.d_out.p;
+            if (int r = log_verify_impl(*w, sl.d_in.p, std::min(CH, log_bytes - i * CH), checksum, ev, ev_cap, &n,
+                                        w->stream, false))
+                return r;
+            if (n && total + n <= cap) {  // past cap: keep counting for *n_events, copy nothing
+                JL_HIP(jlk::launch_event_rebase((jlk::LogEvent *)ev, n, i * CH, w->stream));
+                JL_HIP(hipMemcpyAsync(events + total, ev, n * sizeof(jl_log_event), hipMemcpyDeviceToHost, w->stream));
+            }
+            total += n;
+            return JL_OK;
+        });
+    *n_events = total;
+    if (rc) return rc;
+    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
     return JL_OK;
 }
 

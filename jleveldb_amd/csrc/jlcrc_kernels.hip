@@ -842,6 +842,20 @@ hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, con
     return hipGetLastError();
 }
 
+// Chunked host log verification (jl_log_verify): a chunk's events carry offsets
+// relative to the chunk; this moves them to file offsets before the copy out.
+__global__ void event_rebase_kernel(LogEvent *__restrict__ ev, uint64_t n, uint64_t base) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        ev[i].offset += base;
+}
+
+hipError_t launch_event_rebase(LogEvent *ev, uint64_t n, uint64_t base, hipStream_t st) {
+    if (n == 0 || base == 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(event_rebase_kernel, dim3(grid), dim3(256), 0, st, ev, n, base);
+    return hipGetLastError();
+}
+
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st) {
     hipLaunchKernelGGL(read_stream_kernel, dim3(grid), dim3(256), 0, st, (const uint8_t *)src, bytes, sink);
     return hipGetLastError();

@@ -176,6 +176,7 @@ hipError_t launch_logstream_compact(const LogStreamArgs &A, const uint64_t *star
                                     hipStream_t st);
 hipError_t launch_log_copy(const uint8_t *src, const uint64_t *frag_src_off, const uint64_t *frag_hdr_off,
                            const uint32_t *frag_len, uint64_t n_frags, uint8_t *log, uint64_t *pay_off, hipStream_t st);
+hipError_t launch_event_rebase(LogEvent *ev, uint64_t n, uint64_t base, hipStream_t st);
 hipError_t launch_read_stream(const void *src, uint64_t bytes, uint32_t *sink, int grid, hipStream_t st);
 hipError_t launch_fill_random(void *dst, uint64_t bytes, uint64_t seed, uint64_t first_word, hipStream_t st);
 

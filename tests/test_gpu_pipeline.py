@@ -1,0 +1,166 @@
+"""Host-memory entry points through the chunked double-buffered pipeline.
+
+jl_log_verify, jl_table_verify, jl_crc32c_batch and jl_crc32c_fixed stream
+host input in JL_STREAM_CHUNK_BYTES (64 MiB) chunks; these inputs span several
+chunks (with a partial last one) and are checked against the oracle
+(`oracle.log_events` restates J/db/LogReader.java:297-383, `oracle.batch`
+J/util/Crc32C.java:85-93) for every way host memory reaches the device:
+pageable staged through pinned buffers, pageable pinned for the call
+(hipHostRegister), and pinned tensors.  Also: offsets that do not ascend (one
+window), a block larger than a chunk, corruption on both sides of a chunk
+boundary, and several threads calling at once (per-thread workspaces).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from jleveldb_amd import workloads as wl
+
+pytestmark = pytest.mark.gpu
+
+CH = 64 << 20
+SEED = 0x4A4C4442
+MODES = ["staged", "registered", "pinned"]
+
+
+def _as_mode(jl, engine_options, a, mode):
+    """The host buffer for `mode` (and the engine options it needs)."""
+    import torch
+
+    engine_options(jl.OPT_HOST_REGISTER, 1 if mode == "registered" else 0)
+    if mode == "pinned":
+        t = torch.empty(a.size, dtype=torch.uint8, pin_memory=True)
+        t.numpy()[:] = a
+        return t
+    return a
+
+
+def _live(ev):
+    ev = ev[ev["kind"] != 0]
+    return np.stack([ev["offset"], ev["length"].astype(np.uint64), ev["type"].astype(np.uint64),
+                     ev["kind"].astype(np.uint64)])
+
+
+@pytest.fixture(scope="module")
+def log_image(gpu, jl):
+    """~200 MiB log (3 full chunks + a partial one ending in a short block) of
+    mixed 1 B - 100 KiB records written by the product LogWriter, with flips in
+    the last block of chunk 0, the first of chunk 1 and one inside chunk 2."""
+    import torch
+
+    lens = wl.c5_lengths(True, target=200 << 20, seed=SEED)
+    plan = jl.log_layout(wl.packed_offsets(lens), lens)
+    src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(src, SEED + 9)
+    log = jl.log_emit_dev(src, plan).cpu().numpy().copy()
+    nb = log.size
+    assert nb > 3 * CH and nb % 32768 != 0
+    for at in (CH - 32768 + 9_000, CH + 5_000, 2 * CH + 777_777):
+        log[at] ^= 0x10
+    return log
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("checksum", [0, 1, 3])
+def test_log_verify_chunked(jl, oracle, engine_options, log_image, mode, checksum):
+    buf = _as_mode(jl, engine_options, log_image, mode)
+    got = jl.log_verify(buf, checksum)
+    want = oracle.log_events(log_image, checksum=bool(checksum))
+    g, w = _live(got), _live(want)
+    assert g.shape == w.shape and np.array_equal(g, w)
+    if checksum:  # the flips are seen (bad crc or bad length), as the oracle sees them
+        assert int(np.isin(w[3], [jl.LOG_BAD_CRC, jl.LOG_BAD_LENGTH]).sum()) >= 1
+
+
+def test_log_verify_capacity(jl, log_image):
+    """A short event array: JL_ERR_CAPACITY with the full count."""
+    import ctypes
+
+    ev = np.zeros(1000, dtype=jl.LOG_EVENT_DTYPE)
+    n = ctypes.c_uint64(0)
+    rc = jl.lib().jl_log_verify(log_image.ctypes.data, log_image.size, 1, ev.ctypes.data, 1000, ctypes.byref(n))
+    assert rc == -5 and n.value == jl.log_verify(log_image).size
+
+
+@pytest.fixture(scope="module")
+def arena():
+    """~160 MiB arena of C3-shaped blocks plus one 70 MiB block (a chunk of its own)."""
+    rng = np.random.default_rng(SEED)
+    lens = wl.c3_lengths(9000, SEED)
+    lens = np.concatenate([lens[:4000], np.array([70 << 20], np.uint32), lens[4000:]])
+    offs = wl.packed_offsets(lens)
+    data = rng.integers(0, 256, int(lens.sum(dtype=np.uint64)) + 4096, dtype=np.uint8)
+    return data, offs, lens
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_batch_chunked(jl, oracle, engine_options, arena, mode):
+    data, offs, lens = arena
+    assert data.size > 2 * CH
+    buf = _as_mode(jl, engine_options, data, mode)
+    init = (np.arange(offs.size, dtype=np.uint32) * 2654435761).astype(np.uint32)
+    sfx = (np.arange(offs.size) % 7).astype(np.uint8)
+    assert np.array_equal(jl.crc32c_batch(buf, offs, lens), oracle.batch(data, offs, lens, threads=8))
+    assert np.array_equal(jl.crc32c_batch(buf, offs, lens, init=init, suffix=sfx),
+                          oracle.batch(data, offs, lens, init=init, suffix=sfx, threads=8))
+
+
+def test_batch_unordered(jl, oracle, arena):
+    data, offs, lens = arena
+    perm = np.random.default_rng(3).permutation(offs.size)
+    o, ln = offs[perm], lens[perm]
+    assert np.array_equal(jl.crc32c_batch(data, o, ln), oracle.batch(data, o, ln, threads=8))
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_table_verify_chunked(jl, oracle, engine_options, mode):
+    """A synthetic ~150 MiB 'table': blocks with valid 5-byte trailers, three of
+    them corrupted (one on each side of the 64 MiB chunk boundary)."""
+    rng = np.random.default_rng(SEED + 1)
+    sizes = rng.integers(1, 1 << 17, 2400).astype(np.uint32)
+    offs = wl.packed_offsets(sizes + 5)
+    data = rng.integers(0, 256, int(offs[-1]) + int(sizes[-1]) + 5 + 100, dtype=np.uint8)
+    crc = oracle.batch(data, offs, sizes + 1, flags=1, threads=8)  # crc of block || type, masked
+    for i in range(sizes.size):
+        p = int(offs[i]) + int(sizes[i]) + 1
+        data[p:p + 4] = np.frombuffer(int(crc[i]).to_bytes(4, "little"), np.uint8)
+    k = int(np.searchsorted(offs, CH))  # first block starting past the boundary
+    bad = [5, k - 1, k]
+    for i in bad:
+        data[int(offs[i])] ^= 0x01
+    buf = _as_mode(jl, engine_options, data, mode)
+    st = jl.table_verify(buf, offs, sizes)
+    assert sorted(np.nonzero(st == 0)[0].tolist()) == bad
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_fixed_chunked(jl, oracle, engine_options, mode):
+    data = np.random.default_rng(SEED + 2).integers(0, 256, (2 * CH + (3 << 20)), dtype=np.uint8)
+    buf = _as_mode(jl, engine_options, data, mode)
+    assert np.array_equal(jl.crc32c_fixed(buf, 4096), oracle.fixed(data, 4096, data.size // 4096, threads=8))
+
+
+def test_concurrent_callers(jl, oracle, arena, log_image):
+    """Four threads at once on the host entry points: each gets its own workspace."""
+    data, offs, lens = arena
+    want_b = oracle.batch(data, offs, lens, threads=8)
+    want_l = _live(oracle.log_events(log_image))
+    errs = []
+
+    def work(t):
+        try:
+            for _ in range(3):
+                if t % 2:
+                    assert np.array_equal(jl.crc32c_batch(data, offs, lens), want_b)
+                else:
+                    assert np.array_equal(_live(jl.log_verify(log_image)), want_l)
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(f"thread {t}: {e!r}")
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
