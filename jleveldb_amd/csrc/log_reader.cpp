@@ -17,15 +17,15 @@ constexpr uint64_t kHeaderSize = 7;     // LogFormat.kHeaderSize, :54
 enum { kZero = 0, kFull = 1, kFirst = 2, kMiddle = 3, kLast = 4, kEof = 5, kBadRecord = 6 };
 
 struct Reader {
-    const uint8_t *file;
-    uint64_t file_size, file_pos = 0;
-    const jl_log_event *ev;
-    uint64_t n_ev, cursor = 0;
-    uint64_t initial_offset;
+    const uint8_t *file = nullptr;
+    uint64_t file_size = 0, file_pos = 0;
+    const jl_log_event *ev = nullptr;
+    uint64_t n_ev = 0, cursor = 0;
+    uint64_t initial_offset = 0;
     uint64_t buf_size = 0;  // bytes left in `buffer` (the current block)
     bool eof = false;
     uint64_t last_record_offset = 0, end_of_buffer_offset = 0;
-    bool resyncing;
+    bool resyncing = false;
     std::vector<jl_log_report> reports;
     bool sync_error = false;
 
@@ -112,7 +112,12 @@ extern "C" int jl_log_read_records(const uint8_t *log, uint64_t log_bytes, int c
         if (r) return r;
         ev.resize(n_ev);
     }
-    Reader R{log, log_bytes, 0, ev.data(), ev.size(), 0, initial_offset};
+    Reader R;
+    R.file = log;
+    R.file_size = log_bytes;
+    R.ev = ev.data();
+    R.n_ev = ev.size();
+    R.initial_offset = initial_offset;
     R.resyncing = initial_offset > 0;
 
     if (R.last_record_offset < R.initial_offset) {  // skipToInitialBlock, :263-289
