@@ -184,7 +184,7 @@ def secondary_c3(dev, stream, steps, warmup, cpu=True):
     return res
 
 
-def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
+def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True, host_copy=True):
     """Config C5: streaming WAL verification over 2^17 x 32 KiB log blocks (4 GiB).
 
     The log is produced on the device by the product's batched LogWriter
@@ -229,6 +229,8 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True):
     _, ms2 = timed(fn2, steps, warmup, stream)
     res["fused"] = {"GiB_per_s": round(nb / (ms2 / steps / 1e3) / GIB, 1), "ms_per_step": round(ms2 / steps, 3),
                     "events_equal": bool(same)}
+    if not host_copy:
+        return res
     host = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
     host.copy_(log)
     del log, events
