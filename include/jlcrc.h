@@ -138,9 +138,11 @@ int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t 
                         const uint32_t *d_init, const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out,
                         void *stream);
 
-/* Host-memory form of jl_crc32c_batch_dev: stages base[0, base_bytes) and the
- * descriptors through pinned buffers to the device, runs the kernel, copies the
- * results back and returns when out[] is filled. */
+/* Host-memory form of jl_crc32c_batch_dev: streams the blocks to the device
+ * and returns when out[] is filled.  With ascending offsets the blocks go in
+ * chunks of <= JL_STREAM_CHUNK_BYTES of arena (double-buffered, only the bytes
+ * the blocks cover are copied); otherwise one window spanning all of them.
+ * Every block must lie in [0, base_bytes) (JL_ERR_INVALID otherwise). */
 int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *off, const uint32_t *len,
                     const uint32_t *init, const uint8_t *suffix, uint64_t n, uint32_t flags, uint32_t *out);
 
