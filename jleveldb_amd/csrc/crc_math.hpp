@@ -275,8 +275,12 @@ inline std::vector<uint32_t> build_lds_image_logstream() {
 //   [528,1552)  U_j[v] = slice4^-1(v << 8j), j = 0..3     (seed of an arbitrary init)
 //   [1552,5648) Z_k = z^(2^k), k = 0..31, nibble tables (8 x 16 each): the state
 //               shift by 2^k zero bytes (folding the chunks of a split block)
+//   [5648, +256*128)  ZW_a = z^(128 a), a = 0..255, nibble tables (log chunk fold)
+//   [.., +128*128)    ZB_b = z^b, b = 0..127, nibble tables
 constexpr size_t kAuxZpow = 1552;
-constexpr size_t kAuxDwords = kAuxZpow + 32 * 128;
+constexpr size_t kAuxZW = kAuxZpow + 32 * 128;
+constexpr size_t kAuxZB = kAuxZW + 256 * 128;
+constexpr size_t kAuxDwords = kAuxZB + 128 * 128;
 inline std::vector<uint32_t> build_aux() {
     const Tables &T = tables();
     std::vector<uint32_t> aux(kAuxDwords, 0);
@@ -292,7 +296,7 @@ inline std::vector<uint32_t> build_aux() {
     // z^(2^k) by repeated squaring of the 32x32 GF(2) matrix of z (column b = z(e_b))
     uint32_t col[32], sq[32];
     for (int b = 0; b < 32; b++) col[b] = T.z(1u << b);
-    auto apply = [](const uint32_t *m, uint32_t v) {
+    auto apply = [](const uint32_t *m, uint32_t v) {  // column b of m = image of bit b
         uint32_t r = 0;
         for (int b = 0; b < 32; b++)
             if ((v >> b) & 1u) r ^= m[b];
@@ -303,6 +307,25 @@ inline std::vector<uint32_t> build_aux() {
             for (uint32_t v = 0; v < 16; v++) aux[kAuxZpow + 128 * k + 16 * p + v] = apply(col, v << (4 * p));
         for (int b = 0; b < 32; b++) sq[b] = apply(col, col[b]);
         for (int b = 0; b < 32; b++) col[b] = sq[b];
+    }
+    // z^b (b < 128) and z^(128 a) (a < 256) by repeated multiplication
+    uint32_t z1[32], zb[32], z128[32], zw[32];
+    for (int b = 0; b < 32; b++) z1[b] = zb[b] = zw[b] = 1u << b;
+    auto put = [&](size_t at, const uint32_t *m) {
+        for (int p = 0; p < 8; p++)
+            for (uint32_t v = 0; v < 16; v++) aux[at + 16 * p + v] = apply(m, v << (4 * p));
+    };
+    for (int b = 0; b < 32; b++) z1[b] = T.z(1u << b);
+    for (int i = 0; i < 128; i++) {
+        put(kAuxZB + 128 * (size_t)i, zb);
+        for (int b = 0; b < 32; b++) sq[b] = apply(z1, zb[b]);
+        for (int b = 0; b < 32; b++) zb[b] = sq[b];
+    }
+    for (int b = 0; b < 32; b++) z128[b] = zb[b];  // z^128
+    for (int a = 0; a < 256; a++) {
+        put(kAuxZW + 128 * (size_t)a, zw);
+        for (int b = 0; b < 32; b++) sq[b] = apply(z128, zw[b]);
+        for (int b = 0; b < 32; b++) zw[b] = sq[b];
     }
     return aux;
 }

@@ -123,6 +123,7 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 template <int MODE>
 struct GV4 {
     static constexpr bool VERIFY = MODE == MODE_TABLE_VERIFY || MODE == MODE_LOG_VERIFY;
+    static constexpr bool LOGC = MODE == MODE_LOG_CHUNK;  // stored crc in the descriptor: no side entry
 };
 
 // Per-lane view of a round's descriptor (group q = lane >> 3).
@@ -131,6 +132,7 @@ struct RoundView {
     uint32_t d;    // per lane: tail pad
     uint32_t idx;  // per lane (kGNull: no result)
     uint32_t K;    // wave-uniform
+    uint32_t stored, seed;  // MODE_LOG_CHUNK: per lane, the group's stored crc and seed flag
 };
 
 __device__ __forceinline__ uint32_t sel8(uint32_t q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
@@ -140,8 +142,11 @@ __device__ __forceinline__ uint32_t sel8(uint32_t q, uint32_t a0, uint32_t a1, u
     return lo;
 }
 
+template <int MODE>
 __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, uint32_t q) {
     RoundView v;
+    v.stored = 0;
+    v.seed = 0;
     if (A.desc) {
         // the round's 8 descriptors (128 B) with two scalar loads: SMEM/lgkmcnt, so the
         // hand-counted vmcnt ring never sees them (a compiler-emitted vector load here
@@ -172,6 +177,12 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, ui
         v.p = ((uint64_t)(hi & 0xffffffu) << 32) | lo;
         v.d = hi >> 24;
         v.idx = sel8(q, ix[0], ix[1], ix[2], ix[3], ix[4], ix[5], ix[6], ix[7]);
+        if constexpr (GV4<MODE>::LOGC) {  // pd = offset (40 bits) | K << 40 | seed << 48 | d << 56; K word = stored crc
+            v.K = (w[1] >> 8) & 0xffu;
+            v.p = (uint64_t)(uintptr_t)A.P.base + (((uint64_t)(hi & 0xffu) << 32) | lo);
+            v.seed = (hi >> 16) & 1u;
+            v.stored = sel8(q, w[3], w[7], w[11], w[15], w[19], w[23], w[27], w[31]);
+        }
     } else {  // 128-B aligned base and stride (run_gv4): f = d = 0
         const uint64_t i = (uint64_t)uni(r) * 8u + q;
         const uint64_t ie = i < A.P.n ? i : (uint64_t)uni(r) * 8u;
@@ -199,7 +210,8 @@ __device__ __forceinline__ void desc_issue(const GV4Args &A, uint32_t r, uint32_
     else
         asm volatile("global_load_dwordx4 " JL_GV4_DQ0 ", %0, off" ::"v"(a) : "memory", JL_GV4_DR0);
 }
-__device__ __forceinline__ RoundView desc_read(uint32_t set) {
+template <int MODE>
+__device__ __forceinline__ RoundView desc_read(const GV4Args &A, uint32_t set) {
     uint32_t lo, hi, ix, k;
     if (set)
         asm volatile(JL_GV4_DMOV1
@@ -216,6 +228,14 @@ __device__ __forceinline__ RoundView desc_read(uint32_t set) {
     v.d = hi >> 24;
     v.idx = ix;
     v.K = (uint32_t)__builtin_amdgcn_readlane((int)k, 0);
+    v.stored = 0;
+    v.seed = 0;
+    if constexpr (GV4<MODE>::LOGC) {
+        v.K = (uint32_t)__builtin_amdgcn_readlane((int)((hi >> 8) & 0xffu), 0);
+        v.p = (uint64_t)(uintptr_t)A.P.base + (((uint64_t)(hi & 0xffu) << 32) | lo);
+        v.seed = (hi >> 16) & 1u;
+        v.stored = k;
+    }
     return v;
 }
 
@@ -242,10 +262,10 @@ struct GPF {
         const uint32_t q = lane >> 3, l = lane & 7u;  // group, lane in group
         RoundView v;
         if (vec) {
-            v = desc_read(k & 1u);
+            v = desc_read<MODE>(A, k & 1u);
         } else {
             for (;;) {  // K == 0 rounds (empty blocks, results already written) are skipped
-                v = round_view(A, r, q);
+                v = round_view<MODE>(A, r, q);
                 if (uni(v.K) != 0u) break;
                 r = uni(r + W);
                 if (r >= R) return;
@@ -353,7 +373,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     RoundView cv;
     for (;;) {
         if (cr >= R) return;
-        cv = round_view(A, cr, q);
+        cv = round_view<MODE>(A, cr, q);
         if (uni(cv.K) != 0u) break;
         cr = uni(cr + waves);
     }
@@ -424,6 +444,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                     lds_at(lds, kG4UByte + 3072u + ((y >> 24) << 2));
             }
             if (MODE == MODE_CRC && cv.idx >= kGPart) W = 0u;  // chunk of a split block: from state 0
+            if constexpr (GV4<MODE>::LOGC) W = cv.seed ? A.seed0 : 0u;  // record chunks after the first: from 0
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int t = (int)(16u * l + 4u * j) - (int)f;  // dword start relative to p
@@ -484,7 +505,14 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                 A.P.dbg[4 + 4 * slot] = cv.idx;
             }
         } else if (l == 0u && cv.idx != kGNull) {
-            if (MODE == MODE_CRC) {
+            if constexpr (GV4<MODE>::LOGC) {
+                if (cv.idx >= kGPart) {
+                    A.parts[cv.idx - kGPart] = raw;
+                } else if (m != cv.stored) {  // rare: first_bad[block] = min(header offset in the block)
+                    const uint64_t h = p - 6u - (uint64_t)(uintptr_t)A.P.base;
+                    atomicMin(A.P.out32 + (h >> 15), (uint32_t)(h & 32767u));
+                }
+            } else if (MODE == MODE_CRC) {
                 if (cv.idx >= kGPart) A.parts[cv.idx - kGPart] = raw;
                 else A.P.out32[cv.idx] = (A.P.flags & 1u) ? m : crc;
             } else {
@@ -510,12 +538,12 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         if (vec) {
             cr = uni(cr + waves);
             if (cr >= R) return false;
-            cv = desc_read(ck & 1u);
+            cv = desc_read<MODE>(A, ck & 1u);
         } else {
             for (;;) {
                 cr = uni(cr + waves);
                 if (cr >= R) return false;
-                cv = round_view(A, cr, q);
+                cv = round_view<MODE>(A, cr, q);
                 if (uni(cv.K) != 0u) break;
             }
         }

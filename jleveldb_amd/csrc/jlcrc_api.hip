@@ -25,6 +25,7 @@ static_assert(jlmath::kLSMaskDword * 4 == jlk::kLSMaskByte && jlmath::kLSStageDw
                   jlmath::kLSLaneDword * 4 == jlk::kLSLaneByte && jlmath::kLSShiftDword * 4 == jlk::kLSShiftByte &&
                   jlmath::kLSEDword * 4 == jlk::kLSEByte,
               "log-stream image layout mismatch");
+static_assert(jlmath::kAuxZW == 5648 && jlmath::kAuxZB == 5648 + 256 * 128, "aux layout mismatch (log_chunks.hip)");
 static_assert(jlmath::kV4SlotDword == jlk::kV4SlotDword && jlmath::kV4UDword * 4 == jlk::kV4U4Byte, "v4 image layout mismatch");
 
 namespace {
@@ -104,12 +105,12 @@ struct Slot {
 // a thread's first call; released when the thread exits or by jl_shutdown.
 struct Workspace {
     hipStream_t stream = nullptr;  // compute stream of the host-memory entry points
-    DevBuf ws_cnt, ws_start, ws_slot, ws_off, ws_len, ws_ok, ws_tmp;  // two-pass log verify
+    DevBuf ws_lc, ws_slot, ws_desc, ws_big, ws_part, ws_tmp;  // chunked log verify (log_chunks.hip)
     DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
     Slot slot[2];
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
-        for (DevBuf *b : {&ws_cnt, &ws_start, &ws_slot, &ws_off, &ws_len, &ws_ok, &ws_tmp, &ws_ls, &ws_lsev})
+        for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_ls, &ws_lsev})
             b->release();
         for (Slot &sl : slot) {
             if (sl.st) (void)hipStreamSynchronize(sl.st);
@@ -507,6 +508,7 @@ static hipError_t gv4_launch(const jlk::GV4Args &A, hipStream_t st) {
     switch (A.P.mode) {
     case jlk::MODE_CRC: return jlk::launch_gv4_m<jlk::MODE_CRC>(img, A, ctx().d_zero, grid, st);
     case jlk::MODE_TABLE_VERIFY: return jlk::launch_gv4_m<jlk::MODE_TABLE_VERIFY>(img, A, ctx().d_zero, grid, st);
+    case jlk::MODE_LOG_CHUNK: return jlk::launch_gv4_m<jlk::MODE_LOG_CHUNK>(img, A, ctx().d_zero, grid, st);
     default: return jlk::launch_gv4_m<jlk::MODE_LOG_VERIFY>(img, A, ctx().d_zero, grid, st);
     }
 }
@@ -1077,6 +1079,115 @@ static int log_verify_stream(Workspace &c, const void *d_log, uint64_t log_bytes
     return JL_OK;
 }
 
+// Chunked log verification (log_chunks.hip): walk -> scans -> rounds setup ->
+// build -> crc_gv4_kernel<MODE_LOG_CHUNK> -> combine -> apply, stream-ordered,
+// one synchronisation at the end (the event count and the overflow flags).
+// The fast mode sizes the round table for at most kLCSlots events per 32 KiB
+// block (records of ~512 B and up); a log with a block of more events sets
+// *redo and the caller runs the exact mode, which reads the chunk totals back
+// after the walk and re-walks the blocks past their slots.
+static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum, int exact,
+                             jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo) {
+    *redo = false;
+    if (log_bytes >= (1ull << 40)) return fail(JL_ERR_INVALID, "jl_log_verify: log larger than 1 TiB");
+    const uint64_t nb = (log_bytes + 32767) / 32768, nwg = (nb + jlk::kLCWalkThreads - 1) / jlk::kLCWalkThreads;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t hn = jlk::kLCCounters * nwg + 1;
+    const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
+                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCWin + 1) * 4), o_flag = o_fb + al(nb * 4),
+                 o_end = o_flag + 256;
+    JL_HIP(c.ws_lc.ensure(o_end));
+    JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * sizeof(jlk::LCSlot)));
+    char *ws = (char *)c.ws_lc.p;
+    jlk::LCArgs A;
+    memset(&A, 0, sizeof(A));
+    A.log = (const uint8_t *)d_log;
+    A.size = log_bytes;
+    A.n_blocks = (uint32_t)nb;
+    A.n_wg = (uint32_t)nwg;
+    A.exact = exact;
+    A.checksum = checksum ? 1 : 0;
+    A.slots = (jlk::LCSlot *)c.ws_slot.p;
+    A.count = (uint32_t *)(ws + o_cnt);
+    A.start = (uint64_t *)(ws + o_start);
+    A.hist = (uint32_t *)(ws + o_hist);
+    A.hscan = (uint32_t *)(ws + o_hscan);
+    A.rstart = (uint32_t *)(ws + o_rs);
+    A.first_bad = (uint32_t *)(ws + o_fb);
+    A.overflow = (uint32_t *)(ws + o_flag);
+    A.ev = (jlk::LogEvent *)d_events;
+    A.ev_cap = d_events ? cap : 0;
+    A.aux = ctx().d_aux;
+    JL_HIP(hipMemsetAsync(A.count + nb, 0, 4, st));  // count[nb] = 0: start[nb] is the total
+    JL_HIP(hipMemsetAsync(A.hist + hn - 1, 0, 4, st));
+    JL_HIP(hipMemsetAsync(A.overflow, 0, 8, st));
+    if (checksum) JL_HIP(hipMemsetAsync(A.first_bad, 0xff, nb * 4, st));
+    JL_HIP(jlk::launch_lc_walk(A, st));
+    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
+    size_t t1 = 0, t2 = 0;
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, it, A.start, (int)(nb + 1), st));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, A.hist, A.hscan, (int)hn, st));
+    JL_HIP(c.ws_tmp.ensure(std::max(t1, t2)));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t1, it, A.start, (int)(nb + 1), st));
+    if (checksum) JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t2, A.hist, A.hscan, (int)hn, st));
+    // capacities of the round table, the multi-chunk records and their chunk states
+    uint64_t chunks, bigs, parts;
+    if (exact) {  // read the totals back
+        uint32_t h[3] = {0, 0, 0};
+        if (checksum) {
+            JL_HIP(hipMemcpyAsync(&h[0], A.hscan + jlk::kLCBig * nwg, 4, hipMemcpyDeviceToHost, st));
+            JL_HIP(hipMemcpyAsync(&h[1], A.hscan + jlk::kLCPart * nwg, 4, hipMemcpyDeviceToHost, st));
+            JL_HIP(hipMemcpyAsync(&h[2], A.hscan + jlk::kLCCounters * nwg, 4, hipMemcpyDeviceToHost, st));
+            JL_HIP(hipStreamSynchronize(st));
+        }
+        chunks = h[0];
+        bigs = h[1] - h[0];
+        parts = h[2] - h[1];
+    } else {  // <= kLCSlots records a block, and a block's bytes bound its extra chunks
+        chunks = nb * (jlk::kLCSlots + 10);
+        bigs = nb * 8;
+        parts = nb * 17;
+    }
+    A.round_cap = chunks / 8 + jlk::kLCWin + 1;
+    A.big_cap = bigs + 1;
+    A.part_cap = parts + 1;
+    if (checksum) {
+        JL_HIP(c.ws_desc.ensure(A.round_cap * 8 * sizeof(jlk::GDesc)));
+        JL_HIP(c.ws_big.ensure(A.big_cap * sizeof(jlk::LCBig)));
+        JL_HIP(c.ws_part.ensure(A.part_cap * 4));
+        A.desc = (jlk::GDesc *)c.ws_desc.p;
+        A.big = (jlk::LCBig *)c.ws_big.p;
+        A.parts = (uint32_t *)c.ws_part.p;
+        JL_HIP(jlk::launch_lc_setup(A, st));
+    }
+    JL_HIP(jlk::launch_lc_build(A, st));
+    if (checksum) {
+        jlk::GV4Args G;
+        memset(&G, 0, sizeof(G));
+        G.P = base_params(d_log, nb, jlk::MODE_LOG_CHUNK);
+        G.P.out32 = A.first_bad;
+        G.desc = A.desc;
+        G.n_rounds = A.rstart + jlk::kLCWin;
+        G.seed0 = jlmath::slice4_inv(0xffffffffu);
+        G.parts = A.parts;
+        JL_HIP(gv4_launch(G, st));
+        JL_HIP(jlk::launch_lc_combine(A, st));
+        JL_HIP(jlk::launch_lc_apply(A, st));
+    }
+    uint64_t total = 0;
+    uint32_t over[2] = {0, 0};
+    JL_HIP(hipMemcpyAsync(&total, A.start + nb, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipMemcpyAsync(over, A.overflow, 8, hipMemcpyDeviceToHost, st));
+    JL_HIP(hipStreamSynchronize(st));
+    if (over[0] && !exact) {
+        *redo = true;
+        return JL_OK;
+    }
+    if (over[1]) return fail(JL_ERR_HIP, "jl_log_verify: internal capacity exceeded");
+    *n_events = total;
+    return JL_OK;
+}
+
 // Verifies d_log[0, log_bytes) on `st` with the calling thread's scratch `c`.
 // *n_events is known on return (the event count is read back); with sync_end
 // the events are complete too, else they complete in stream order (the host
@@ -1090,43 +1201,19 @@ static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, 
         if (int r = log_verify_stream(c, d_log, log_bytes, d_events, cap, n_events, st, &fallback)) return r;
         if (!fallback) return JL_OK;
     }
-    const uint64_t nb = (log_bytes + 32767) / 32768;
     *n_events = 0;
-    if (nb == 0) return JL_OK;
-    JL_HIP(c.ws_cnt.ensure((nb + 1) * 8));  // cnt[nb] = 0: the exclusive scan's start[nb] is the total
-    JL_HIP(c.ws_start.ensure((nb + 1) * 8));
-    JL_HIP(c.ws_slot.ensure(nb * jlk::kLogSlots * sizeof(jlk::LogSlot)));
-    uint64_t *cnt = (uint64_t *)c.ws_cnt.p, *start = (uint64_t *)c.ws_start.p;
-    jlk::LogSlot *slots = (jlk::LogSlot *)c.ws_slot.p;
-    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 0, cnt, nullptr, nullptr, nullptr, nullptr, slots,
-                                st));
-    JL_HIP(hipMemsetAsync(cnt + nb, 0, 8, st));
-    size_t tmp = 0;
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cnt, start, (int)(nb + 1), st));
-    JL_HIP(c.ws_tmp.ensure(tmp));
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, tmp, cnt, start, (int)(nb + 1), st));
-    uint64_t total = 0;  // one copy back: the event count sizes the next buffers
-    JL_HIP(hipMemcpyAsync(&total, start + nb, 8, hipMemcpyDeviceToHost, st));
-    JL_HIP(hipStreamSynchronize(st));
-    *n_events = total;
-    if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
-    if (total == 0) return JL_OK;
-    JL_HIP(c.ws_off.ensure(total * 8));
-    JL_HIP(c.ws_len.ensure(total * 4));
-    JL_HIP(c.ws_ok.ensure(total));
-    JL_HIP(jlk::launch_log_walk((const uint8_t *)d_log, log_bytes, nb, 1, cnt, start, (jlk::LogEvent *)d_events,
-                                (uint64_t *)c.ws_off.p, (uint32_t *)c.ws_len.p, slots, st));
-    if (checksum) {
-        jlk::KParams P = base_params(d_log, total, jlk::MODE_LOG_VERIFY);
-        P.off = (const uint64_t *)c.ws_off.p;
-        P.len = (const uint32_t *)c.ws_len.p;
-        P.out8 = (uint8_t *)c.ws_ok.p;
-        if (int r = run_general(P, st)) return r;
-        // firstbad scratch: the walk's slot workspace is free again (n_blocks words fit in it)
-        JL_HIP(jlk::launch_log_finalize(nb, start, cnt, (const uint8_t *)c.ws_ok.p, (jlk::LogEvent *)d_events, 1, total,
-                                        (unsigned long long *)c.ws_slot.p, st));
+    if (log_bytes == 0) return JL_OK;
+    int exact = 0;
+    for (;;) {
+        bool redo = false;
+        if (int r = log_verify_chunks(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, exact, d_events, cap, n_events,
+                                      st, &redo))
+            return r;
+        if (!redo) break;
+        exact = 1;  // a block held more than kLCSlots events: once more with exact sizing
     }
-    if (sync_end) JL_HIP(hipStreamSynchronize(st));
+    if (*n_events > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    (void)sync_end;  // log_verify_chunks ends with a synchronisation (the event count)
     return JL_OK;
 }
 

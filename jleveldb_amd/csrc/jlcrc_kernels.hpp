@@ -22,6 +22,8 @@ enum : int {
     MODE_LOG_VERIFY = 2,    // out8[i] = (LE32 @ ptr-6 == mask(crc))   LogReader.readPhysicalRecord
     MODE_TRAILER = 3,       // out8[5i..] = [type][LE32 mask]          TableBuilder.writeRawBlock
     MODE_LOG_HEADER = 4,    // out8[7i..] = [LE32 mask][LE16 n][type]  LogWriter.emitPhysicalRecord
+    MODE_LOG_CHUNK = 5,     // gv4 only: log record chunks (LDesc below); a failing record
+                            // atomicMin's its header offset into out32[block] (first_bad)
 };
 
 struct KParams {
@@ -49,6 +51,14 @@ struct KParams {
     // offending accesses {block, entry, lane, address}; dbg == null: off
     uint64_t dbg_lo, dbg_hi;
     unsigned long long *dbg;
+};
+
+struct LogEvent {  // layout-identical to jl_log_event
+    uint64_t offset;
+    uint32_t length;
+    uint8_t type;
+    uint8_t kind;
+    uint16_t pad;
 };
 
 // general v4 path (general_v4.hip): group descriptor of the sorted pipeline
@@ -86,6 +96,68 @@ struct GSplit {       // rounds-pipeline state of the block split
 };
 constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 131071 steps: one per round
 
+// ---------------------------------------------------------------------------
+// Chunked log verification (log_chunks.hip + crc_gv4_kernel<MODE_LOG_CHUNK>).
+// Every OK record's crc range [h + 6, h + 7 + len) is cut on the 128-B grid into
+// chunks of at most kLCWin windows; chunks are sorted into rounds of 8 with the
+// same window count K (exact bins 1..kLCWin) with no global atomics: per-
+// workgroup histograms from the walk, one scan, deterministic placement.
+// A record of one chunk is verified in the round's epilogue; the chunks of a
+// longer record leave raw states in parts[] and log_combine_kernel folds them.
+// GDesc fields in this mode (the same 16 B):
+//   pd  = chunk start relative to the log (bits 0..39) | K << 40 | seed << 48 | d << 56
+//         (seed: the chunk holds the record's first byte, W0 is fed before it)
+//   idx = 0 (single-chunk record), kGPart | part index, or kGNull
+//   K   = the record's stored masked crc (single-chunk records)
+constexpr uint32_t kLCWin = 32;          // windows per chunk (4 KiB)
+constexpr uint32_t kLCCounters = 34;     // per workgroup: bins K = 1..32, multi-chunk records, parts
+constexpr uint32_t kLCBig = 32, kLCPart = 33;
+constexpr uint32_t kLCSlots = 64;        // walked events kept per 32 KiB block
+constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
+constexpr uint32_t kLCWalkThreads = 256;   // blocks per walk / build workgroup
+struct LCSlot {       // one walked event (16 B)
+    uint32_t off_len;  // header offset in the block | length << 16
+    uint32_t tk;       // type | kind << 8
+    uint32_t stored;   // stored masked crc (LE32 of header bytes 0..3)
+    uint32_t pad;
+};
+struct LCBig {        // a record of more than one chunk
+    uint64_t p;       // crc range start (h + 6) relative to the log
+    uint32_t n;       // crc range bytes (1 + length)
+    uint32_t stored;
+    uint32_t part0;   // its chunk states parts[part0 .. part0 + J)
+    uint32_t J;
+};
+struct LCArgs {
+    const uint8_t *log;
+    uint64_t size;
+    uint32_t n_blocks, n_wg;
+    int exact;             // 1: blocks with more than kLCSlots events are re-walked
+    int checksum;
+    LCSlot *slots;         // n_blocks * kLCSlots
+    uint32_t *count;       // n_blocks + 1 (count[n_blocks] = 0)
+    uint64_t *start;       // n_blocks + 1: exclusive scan of count
+    uint32_t *hist;        // kLCCounters * n_wg + 1, counter-major (hist[c * n_wg + wg])
+    uint32_t *hscan;       // its exclusive scan
+    uint32_t *rstart;      // kLCWin + 1: first round of every bin; [kLCWin] = rounds
+    uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
+    uint32_t *overflow;    // [0]: a block walked more than kLCSlots events; [1]: a capacity was exceeded
+    GDesc *desc;           // rounds * 8
+    uint64_t round_cap;    // rounds the desc array holds
+    LCBig *big;
+    uint64_t big_cap;
+    uint32_t *parts;
+    uint64_t part_cap;
+    LogEvent *ev;
+    uint64_t ev_cap;
+    const uint32_t *aux;
+};
+hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
+
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)
 // inside the caller's base_bytes
 __host__ __device__ inline bool block_in_range(const KParams &P, uint64_t off, uint32_t n) {
@@ -93,14 +165,6 @@ __host__ __device__ inline bool block_in_range(const KParams &P, uint64_t off, u
     const uint64_t need = (uint64_t)n + (P.mode == MODE_TABLE_VERIFY ? 4u : 0u);
     return off <= P.base_bytes && need <= P.base_bytes - off;
 }
-
-struct LogEvent {  // layout-identical to jl_log_event
-    uint64_t offset;
-    uint32_t length;
-    uint8_t type;
-    uint8_t kind;
-    uint16_t pad;
-};
 
 // study build only (JL_STUDY): the round-1 4 KiB kernels and the chunked general kernel
 hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
