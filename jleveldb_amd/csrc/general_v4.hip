@@ -124,6 +124,8 @@ template <int MODE>
 struct GV4 {
     static constexpr bool VERIFY = MODE == MODE_TABLE_VERIFY || MODE == MODE_LOG_VERIFY;
     static constexpr bool LOGC = MODE == MODE_LOG_CHUNK;  // stored crc in the descriptor: no side entry
+    // a side entry (stored crc / init / suffix chunk) heads every round; never in MODE_LOG_CHUNK
+    __device__ static bool side(const GV4Args &A) { return !LOGC && (VERIFY || A.P.init || A.P.suffix); }
 };
 
 // Per-lane view of a round's descriptor (group q = lane >> 3).
@@ -241,8 +243,7 @@ __device__ __forceinline__ RoundView desc_read(const GV4Args &A, uint32_t set) {
 
 template <int MODE>
 __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
-    const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
-    return K + (side ? 1u : 0u);
+    return K + (GV4<MODE>::side(A) ? 1u : 0u);
 }
 
 
@@ -287,7 +288,10 @@ struct GPF {
         addr = (p & ~(uint64_t)127) + 16u * l;
         // side chunks (16-B aligned, each holding a byte of what is needed): lane 0 / 1 of the group
         uint64_t c0 = pa, c1 = pa;
-        if (GV4<MODE>::VERIFY) {
+        if constexpr (GV4<MODE>::LOGC) {
+            e = 0;
+            return;
+        } else if (GV4<MODE>::VERIFY) {
             const uint64_t sa = MODE == MODE_LOG_VERIFY ? p - 6u : p + n;  // stored crc
             c0 = sa & ~(uint64_t)15;
             c1 = (sa + 3u) & ~(uint64_t)15;
@@ -333,8 +337,7 @@ struct GPF {
     }
     __device__ __forceinline__ uint64_t next_raw(const GV4Args &A, uint32_t lane) {
         if (r >= R) return dummy;  // past the wave's last round: keep the ring count exact
-        const bool has_side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
-        const uint32_t e0 = has_side ? 1u : 0u;
+        const uint32_t e0 = GV4<MODE>::side(A) ? 1u : 0u;
         uint64_t a;
         if (e >= e0) {
             a = addr;
@@ -377,8 +380,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         if (uni(cv.K) != 0u) break;
         cr = uni(cr + waves);
     }
-    const bool side = GV4<MODE>::VERIFY || A.P.init || A.P.suffix;
-    const uint32_t e0 = side ? 1u : 0u;
+    const uint32_t e0 = GV4<MODE>::side(A) ? 1u : 0u;
     uint32_t zero_v;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
 
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             // ---- step 0: zero the front pad, feed the seed word W as the 4 bytes before p
             // seed word of this block
             uint32_t W = A.seed0;
-            if (!GV4<MODE>::VERIFY && A.P.init) {
+            if (!GV4<MODE>::VERIFY && !GV4<MODE>::LOGC && A.P.init) {
                 // init[idx] from lane 0's side chunk, broadcast to the group's 8 lanes
                 const uint64_t ia = (uint64_t)(uintptr_t)(A.P.init + (cv.idx == kGNull ? 0u : cv.idx));
                 const uint32_t k = (uint32_t)(ia >> 2) & 3u;
@@ -488,7 +490,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         const uint32_t h3 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.w, 0x101, 0xf, 0xf, false);
         const uint64_t p = cv.p;
         const uint32_t raw = st;  // chunk groups of a split block report the raw state
-        if (!GV4<MODE>::VERIFY && A.P.suffix) {
+        if (!GV4<MODE>::VERIFY && !GV4<MODE>::LOGC && A.P.suffix) {
             const uint64_t sa = (uint64_t)(uintptr_t)(A.P.suffix + (cv.idx == kGNull ? 0u : cv.idx));
             const uint32_t k = (uint32_t)(sa >> 2) & 3u;
             const uint32_t dw = k & 2u ? (k & 1u ? h3 : h2) : (k & 1u ? h1 : h0);

@@ -1090,56 +1090,51 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                              jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo) {
     *redo = false;
     if (log_bytes >= (1ull << 40)) return fail(JL_ERR_INVALID, "jl_log_verify: log larger than 1 TiB");
-    const uint64_t nb = (log_bytes + 32767) / 32768, nwg = (nb + jlk::kLCWalkThreads - 1) / jlk::kLCWalkThreads;
+    const uint64_t nb = (log_bytes + 32767) / 32768, ng = (nb + jlk::kLCGroup - 1) / jlk::kLCGroup;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t hn = jlk::kLCCounters * nwg + 1;
+    const size_t hn = jlk::kLCCounters * ng + 1;
     const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
-                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCWin + 1) * 4), o_flag = o_fb + al(nb * 4),
-                 o_end = o_flag + 256;
+                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_flag = o_fb + al(nb * 4),
+                 o_res = o_flag + 256, o_end = o_res + 256;
     JL_HIP(c.ws_lc.ensure(o_end));
-    JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * sizeof(jlk::LCSlot)));
+    JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
     char *ws = (char *)c.ws_lc.p;
     jlk::LCArgs A;
     memset(&A, 0, sizeof(A));
     A.log = (const uint8_t *)d_log;
     A.size = log_bytes;
     A.n_blocks = (uint32_t)nb;
-    A.n_wg = (uint32_t)nwg;
+    A.n_grp = (uint32_t)ng;
     A.exact = exact;
     A.checksum = checksum ? 1 : 0;
-    A.slots = (jlk::LCSlot *)c.ws_slot.p;
+    A.slots = (uint64_t *)c.ws_slot.p;
     A.count = (uint32_t *)(ws + o_cnt);
     A.start = (uint64_t *)(ws + o_start);
     A.hist = (uint32_t *)(ws + o_hist);
     A.hscan = (uint32_t *)(ws + o_hscan);
     A.rstart = (uint32_t *)(ws + o_rs);
     A.first_bad = (uint32_t *)(ws + o_fb);
-    A.overflow = (uint32_t *)(ws + o_flag);
+    A.cap_flag = (uint32_t *)(ws + o_flag);
+    A.result = (uint64_t *)(ws + o_res);
     A.ev = (jlk::LogEvent *)d_events;
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
-    JL_HIP(hipMemsetAsync(A.count + nb, 0, 4, st));  // count[nb] = 0: start[nb] is the total
-    JL_HIP(hipMemsetAsync(A.hist + hn - 1, 0, 4, st));
-    JL_HIP(hipMemsetAsync(A.overflow, 0, 8, st));
-    if (checksum) JL_HIP(hipMemsetAsync(A.first_bad, 0xff, nb * 4, st));
-    JL_HIP(jlk::launch_lc_walk(A, st));
+    JL_HIP(jlk::launch_lc_walk(A, st));  // initialises count[nb], the hist tail, first_bad, cap_flag
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
     size_t t1 = 0, t2 = 0;
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, it, A.start, (int)(nb + 1), st));
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, A.hist, A.hscan, (int)hn, st));
     JL_HIP(c.ws_tmp.ensure(std::max(t1, t2)));
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t1, it, A.start, (int)(nb + 1), st));
-    if (checksum) JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t2, A.hist, A.hscan, (int)hn, st));
+    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t2, A.hist, A.hscan, (int)hn, st));
     // capacities of the round table, the multi-chunk records and their chunk states
     uint64_t chunks, bigs, parts;
     if (exact) {  // read the totals back
         uint32_t h[3] = {0, 0, 0};
-        if (checksum) {
-            JL_HIP(hipMemcpyAsync(&h[0], A.hscan + jlk::kLCBig * nwg, 4, hipMemcpyDeviceToHost, st));
-            JL_HIP(hipMemcpyAsync(&h[1], A.hscan + jlk::kLCPart * nwg, 4, hipMemcpyDeviceToHost, st));
-            JL_HIP(hipMemcpyAsync(&h[2], A.hscan + jlk::kLCCounters * nwg, 4, hipMemcpyDeviceToHost, st));
-            JL_HIP(hipStreamSynchronize(st));
-        }
+        JL_HIP(hipMemcpyAsync(&h[0], A.hscan + jlk::kLCBig * ng, 4, hipMemcpyDeviceToHost, st));
+        JL_HIP(hipMemcpyAsync(&h[1], A.hscan + jlk::kLCPart * ng, 4, hipMemcpyDeviceToHost, st));
+        JL_HIP(hipMemcpyAsync(&h[2], A.hscan + jlk::kLCOver * ng, 4, hipMemcpyDeviceToHost, st));
+        JL_HIP(hipStreamSynchronize(st));
         chunks = h[0];
         bigs = h[1] - h[0];
         parts = h[2] - h[1];
@@ -1148,7 +1143,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         bigs = nb * 8;
         parts = nb * 17;
     }
-    A.round_cap = chunks / 8 + jlk::kLCWin + 1;
+    A.round_cap = chunks / 8 + jlk::kLCBins + 1;
     A.big_cap = bigs + 1;
     A.part_cap = parts + 1;
     if (checksum) {
@@ -1167,24 +1162,22 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         G.P = base_params(d_log, nb, jlk::MODE_LOG_CHUNK);
         G.P.out32 = A.first_bad;
         G.desc = A.desc;
-        G.n_rounds = A.rstart + jlk::kLCWin;
+        G.n_rounds = A.rstart + jlk::kLCBins;
         G.seed0 = jlmath::slice4_inv(0xffffffffu);
         G.parts = A.parts;
         JL_HIP(gv4_launch(G, st));
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));
     }
-    uint64_t total = 0;
-    uint32_t over[2] = {0, 0};
-    JL_HIP(hipMemcpyAsync(&total, A.start + nb, 8, hipMemcpyDeviceToHost, st));
-    JL_HIP(hipMemcpyAsync(over, A.overflow, 8, hipMemcpyDeviceToHost, st));
+    uint64_t res[3] = {0, 0, 0};  // events, blocks past their slots, capacity flag (lc_finish)
+    JL_HIP(hipMemcpyAsync(res, A.result, sizeof(res), hipMemcpyDeviceToHost, st));
     JL_HIP(hipStreamSynchronize(st));
-    if (over[0] && !exact) {
+    if (res[1] && !exact) {
         *redo = true;
         return JL_OK;
     }
-    if (over[1]) return fail(JL_ERR_HIP, "jl_log_verify: internal capacity exceeded");
-    *n_events = total;
+    if (res[2]) return fail(JL_ERR_HIP, "jl_log_verify: internal capacity exceeded");
+    *n_events = res[0];
     return JL_OK;
 }
 

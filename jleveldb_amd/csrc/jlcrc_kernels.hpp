@@ -110,17 +110,14 @@ constexpr uint32_t kGSoloKey = (1u << 17) - 1;  // sort key of blocks of >= 1310
 //   idx = 0 (single-chunk record), kGPart | part index, or kGNull
 //   K   = the record's stored masked crc (single-chunk records)
 constexpr uint32_t kLCWin = 32;          // windows per chunk (4 KiB)
-constexpr uint32_t kLCCounters = 34;     // per workgroup: bins K = 1..32, multi-chunk records, parts
-constexpr uint32_t kLCBig = 32, kLCPart = 33;
+constexpr uint32_t kLCGroup = 64;        // 32 KiB blocks per walk group (one wave of the walk)
+// chunk bins: (K - 1) * 16 + (d & 15): one round's groups share the epilogue's
+// z^-(4c) and z^-e tables (d = 16a + 4c + e), so its lookups are bank-conflict free
+constexpr uint32_t kLCBins = kLCWin * 16;
+constexpr uint32_t kLCBig = kLCBins, kLCPart = kLCBins + 1, kLCOver = kLCBins + 2;
+constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk records, parts, overflowing blocks
 constexpr uint32_t kLCSlots = 64;        // walked events kept per 32 KiB block
 constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
-constexpr uint32_t kLCWalkThreads = 256;   // blocks per walk / build workgroup
-struct LCSlot {       // one walked event (16 B)
-    uint32_t off_len;  // header offset in the block | length << 16
-    uint32_t tk;       // type | kind << 8
-    uint32_t stored;   // stored masked crc (LE32 of header bytes 0..3)
-    uint32_t pad;
-};
 struct LCBig {        // a record of more than one chunk
     uint64_t p;       // crc range start (h + 6) relative to the log
     uint32_t n;       // crc range bytes (1 + length)
@@ -131,17 +128,18 @@ struct LCBig {        // a record of more than one chunk
 struct LCArgs {
     const uint8_t *log;
     uint64_t size;
-    uint32_t n_blocks, n_wg;
+    uint32_t n_blocks, n_grp;  // 32 KiB blocks, walk groups of kLCGroup blocks
     int exact;             // 1: blocks with more than kLCSlots events are re-walked
     int checksum;
-    LCSlot *slots;         // n_blocks * kLCSlots
+    uint64_t *slots;       // n_blocks * kLCSlots walked events: length | type << 16 | kind << 24 | stored << 32
     uint32_t *count;       // n_blocks + 1 (count[n_blocks] = 0)
     uint64_t *start;       // n_blocks + 1: exclusive scan of count
-    uint32_t *hist;        // kLCCounters * n_wg + 1, counter-major (hist[c * n_wg + wg])
+    uint32_t *hist;        // kLCCounters * n_grp + 1, counter-major (hist[c * n_grp + group])
     uint32_t *hscan;       // its exclusive scan
-    uint32_t *rstart;      // kLCWin + 1: first round of every bin; [kLCWin] = rounds
+    uint32_t *rstart;      // kLCBins + 1: first round of every bin; [kLCBins] = rounds
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
-    uint32_t *overflow;    // [0]: a block walked more than kLCSlots events; [1]: a capacity was exceeded
+    uint32_t *cap_flag;    // set when a capacity was exceeded
+    uint64_t *result;      // [0] events, [1] blocks past their slots, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8
     uint64_t round_cap;    // rounds the desc array holds
     LCBig *big;

@@ -38,6 +38,7 @@ constexpr uint32_t kAuxZBDword = 5648 + 256 * 128;  // jlmath::kAuxZB
 struct LCGeom {
     uint32_t f, K, r, J;
 };
+__device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) { return (K - 1u) * 16u + (d & 15u); }
 __device__ __forceinline__ LCGeom lc_geom(uint64_t pa, uint32_t n) {
     LCGeom g;
     g.f = (uint32_t)(pa & 127u);
@@ -54,6 +55,7 @@ struct LCDecision {
     bool stop;
 };
 __device__ __forceinline__ LCDecision lc_decide(uint64_t rem, bool eof, uint32_t w) {
+    // w: header bytes 3..6 ([crc3][len lo][len hi][type])
     LCDecision d{0u, 0u, 0u, false};
     if (rem < 7) {  // :315-322 (fewer than kHeaderSize bytes left)
         d.kind = (eof && rem > 0) ? 6u : 0u;
@@ -75,57 +77,61 @@ __device__ __forceinline__ LCDecision lc_decide(uint64_t rem, bool eof, uint32_t
 }
 
 __device__ __forceinline__ uint32_t ld_u32u(const uint8_t *p) { return *(const u32u *)p; }
+typedef uint64_t __attribute__((aligned(1))) u64u;
 
-__global__ __launch_bounds__(kLCWalkThreads) void lc_walk_kernel(LCArgs A) {
-    __shared__ uint32_t h[kLCCounters];
-    if (threadIdx.x < kLCCounters) h[threadIdx.x] = 0;
+// Header bytes 0..6 at p ([crc 0..3][len lo][len hi][type]) as one 8-byte load
+// when 8 bytes are left in the block (one memory request on the walk's serial
+// chain), else two dword loads.
+__device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
+    if (rem >= 8) return *(const u64u *)p;
+    return (uint64_t)ld_u32u(p) | ((uint64_t)(ld_u32u(p + 3) >> 8) << 32);
+}
+
+// Walk groups of kLCGroup consecutive blocks, one per wave (4 per workgroup).
+// The walk also initialises what later kernels accumulate into (first_bad,
+// count[n_blocks], the scan's zero tail, cap_flag): no memsets.
+__global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
+    __shared__ uint32_t h[4][kLCCounters];
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t b = (uint64_t)blockIdx.x * kLCWalkThreads + threadIdx.x;
+    const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (b == 0) {
+        A.count[A.n_blocks] = 0;
+        A.hist[(uint64_t)kLCCounters * A.n_grp] = 0;
+        *A.cap_flag = 0;
+    }
     if (b < A.n_blocks) {
+        if (A.checksum) A.first_bad[b] = kLCNone;
         const uint64_t bs = b * 32768u, be = bs + 32768u < A.size ? bs + 32768u : A.size;
         const bool eof = be - bs < 32768u;
         const uint64_t base = (uint64_t)(uintptr_t)A.log;
         uint64_t p = bs;
         uint32_t cnt = 0;
-        // header bytes 0..3 (stored crc) and 3..6 of the next header are loaded
-        // before this record's slot store: vmcnt counts stores too on gfx9, and a
-        // store issued first would put its latency on the walk's serial chain
-        uint32_t w = 0, c = 0;
-        if (be - p >= 7) {
-            w = ld_u32u(A.log + p + 3);
-            c = ld_u32u(A.log + p);
-        }
+        // the next header's load is issued before this record's slot store:
+        // vmcnt counts stores too on gfx9, and a store issued first would put
+        // its latency on the walk's serial chain
+        uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
         for (;;) {
-            const LCDecision d = lc_decide(be - p, eof, w);
+            const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
             if (d.kind == 0) break;  // the block's trailer: no event
             const uint64_t pn = p + 7u + d.length;
-            const uint32_t wc = w, cc = c;
-            if (!d.stop && be - pn >= 7) {
-                w = ld_u32u(A.log + pn + 3);
-                c = ld_u32u(A.log + pn);
-            }
+            const uint32_t stored = (uint32_t)hv;
+            if (!d.stop && be - pn >= 7) hv = lc_header(A.log + pn, be - pn);
             const bool kept = cnt < kLCSlots;
-            if (kept) {
-                uint4 s;
-                s.x = (uint32_t)(p - bs) | (d.length << 16);
-                s.y = d.type | (d.kind << 8);
-                s.z = cc;
-                s.w = 0;
-                reinterpret_cast<uint4 *>(A.slots)[b * kLCSlots + cnt] = s;
-            }
-            (void)wc;
+            if (kept) A.slots[b * kLCSlots + cnt] = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
             // chunk histogram: exactly the chunks lc_build places (in the fast
             // mode only the kept events: a block that overflows its slots makes
-            // the caller re-run in the exact mode)
+            // the caller run the exact mode)
             if (d.kind == 1u && A.checksum && (kept || A.exact)) {
                 const LCGeom g = lc_geom(base + p + 6u, 1u + d.length);
                 if (g.J == 1u) {
-                    atomicAdd(&h[g.K - 1u], 1u);
+                    atomicAdd(&h[wv][lc_bin(g.K, g.r)], 1u);
                 } else {
-                    atomicAdd(&h[kLCWin - 1u], g.J - 1u);
-                    atomicAdd(&h[g.K - kLCWin * (g.J - 1u) - 1u], 1u);
-                    atomicAdd(&h[kLCBig], 1u);
-                    atomicAdd(&h[kLCPart], g.J);
+                    atomicAdd(&h[wv][lc_bin(kLCWin, 0u)], g.J - 1u);
+                    atomicAdd(&h[wv][lc_bin(g.K - kLCWin * (g.J - 1u), g.r)], 1u);
+                    atomicAdd(&h[wv][kLCBig], 1u);
+                    atomicAdd(&h[wv][kLCPart], g.J);
                 }
             }
             cnt++;
@@ -133,46 +139,56 @@ __global__ __launch_bounds__(kLCWalkThreads) void lc_walk_kernel(LCArgs A) {
             p = pn;
         }
         A.count[b] = cnt;
-        if (cnt > kLCSlots) atomicOr(&A.overflow[0], 1u);
+        if (cnt > kLCSlots) atomicAdd(&h[wv][kLCOver], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < kLCCounters) A.hist[(uint64_t)threadIdx.x * A.n_wg + blockIdx.x] = h[threadIdx.x];
+    const uint64_t g0 = (uint64_t)blockIdx.x * 4u;
+    for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) {
+        const uint32_t g = i % 4u, c = i / 4u;  // 4 consecutive groups of one counter: one 16-B run
+        if (g0 + g < A.n_grp) A.hist[(uint64_t)c * A.n_grp + g0 + g] = h[g][c];
+    }
 }
 
-// One wave: rstart[k] = rounds of the bins before k (bin k = chunks of k+1
-// windows, ceil(count/8) rounds each), rstart[kLCWin] = all rounds (clamped to
-// the descriptor capacity, overflow[1] set past it); the missing groups of every
-// bin's last round are marked empty.
-__global__ __launch_bounds__(64) void lc_setup_kernel(LCArgs A) {
-    const uint32_t k = threadIdx.x;
-    const uint64_t nw = A.n_wg;
-    const uint32_t cnt = k < kLCWin ? A.hscan[(k + 1) * nw] - A.hscan[k * nw] : 0u;
+// rstart[k] = rounds of the bins before k (ceil(count/8) rounds each; bin k =
+// chunks of K = k/16 + 1 windows with tail pads d = k mod 16 (mod 16)),
+// rstart[kLCBins] = all rounds (clamped to the descriptor capacity, cap_flag set
+// past it); the missing groups of every bin's last round are marked empty.
+__global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
+    __shared__ uint32_t wsum[kLCBins / 64];
+    const uint32_t k = threadIdx.x, lane = k & 63u, wv = k >> 6;
+    const uint64_t nw = A.n_grp;
+    const uint32_t cnt = A.hscan[(k + 1) * nw] - A.hscan[k * nw];
     const uint32_t rounds = (cnt + 7u) / 8u;
-    uint32_t incl = rounds;  // inclusive wave scan
+    uint32_t incl = rounds;  // inclusive scan: waves, then across the 8 wave sums
     for (uint32_t o = 1; o < 64u; o <<= 1) {
         const uint32_t v = (uint32_t)__shfl_up((int)incl, o);
-        if (k >= o) incl += v;
+        if (lane >= o) incl += v;
     }
-    const uint32_t ex = incl - rounds;
-    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
-    if (k < kLCWin) A.rstart[k] = ex;
+    if (lane == 63u) wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < kLCBins / 64; w++) {
+        before += w < wv ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    const uint32_t ex = before + incl - rounds;
+    A.rstart[k] = ex;
     if (k == 0) {
         const bool over = total > A.round_cap;
-        A.rstart[kLCWin] = over ? (uint32_t)A.round_cap : total;
-        if (over) atomicOr(&A.overflow[1], 1u);
+        A.rstart[kLCBins] = over ? (uint32_t)A.round_cap : total;
+        if (over) atomicOr(A.cap_flag, 1u);
     }
-    if (k < kLCWin && (cnt & 7u)) {
+    if (cnt & 7u) {
         const uint64_t r = (uint64_t)ex + cnt / 8u;
         if (r < A.round_cap)
             for (uint32_t g = cnt & 7u; g < 8u; g++) A.desc[r * 8u + g].idx = kGNull;
     }
 }
 
-__device__ __forceinline__ void lc_put(const LCArgs &A, uint32_t *ctr, uint32_t K, uint64_t prel, uint32_t seed,
-                                       uint32_t d, uint32_t idx, uint32_t stored) {
-    const uint32_t rank = atomicAdd(&ctr[K - 1u], 1u);
-    const uint64_t round = (uint64_t)A.rstart[K - 1u] + rank / 8u;
-    if (round >= A.round_cap) return;  // overflow[1] is set (lc_setup)
+__device__ __forceinline__ void lc_desc(const LCArgs &A, const uint32_t *rs, uint32_t K, uint32_t rank, uint64_t prel,
+                                        uint32_t seed, uint32_t d, uint32_t idx, uint32_t stored) {
+    const uint64_t round = (uint64_t)rs[lc_bin(K, d)] + rank / 8u;
+    if (round >= A.round_cap) return;  // cap_flag is set (lc_setup)
     GDesc g;
     g.pd = (prel & 0xffffffffffull) | ((uint64_t)K << 40) | ((uint64_t)seed << 48) | ((uint64_t)d << 56);
     g.idx = idx;
@@ -180,11 +196,15 @@ __device__ __forceinline__ void lc_put(const LCArgs &A, uint32_t *ctr, uint32_t 
     A.desc[round * 8u + rank % 8u] = g;
 }
 
-// The chunk descriptors of one OK record (crc range at prel, n bytes).
-__device__ __forceinline__ void lc_place(const LCArgs &A, uint32_t *ctr, uint64_t prel, uint32_t n, uint32_t stored) {
+// The chunk descriptors of one OK record (ok false: none).  Ranks come from LDS
+// atomics per lane: with bins by (K, d mod 16) a wave's records spread over many
+// bins, so ballot aggregation would loop once per distinct bin.
+__device__ __forceinline__ void lc_place(const LCArgs &A, uint32_t *ctr, const uint32_t *rs, bool ok, uint64_t prel,
+                                         uint32_t n, uint32_t stored) {
+    if (!ok) return;
     const LCGeom g = lc_geom((uint64_t)(uintptr_t)A.log + prel, n);
     if (g.J == 1u) {
-        lc_put(A, ctr, g.K, prel, 1u, g.r, 0u, stored);
+        lc_desc(A, rs, g.K, atomicAdd(&ctr[lc_bin(g.K, g.r)], 1u), prel, 1u, g.r, 0u, stored);
         return;
     }
     const uint32_t bi = atomicAdd(&ctr[kLCBig], 1u), pi = atomicAdd(&ctr[kLCPart], g.J);
@@ -200,15 +220,17 @@ __device__ __forceinline__ void lc_place(const LCArgs &A, uint32_t *ctr, uint64_
         big.J = g.J;
         A.big[bi] = big;
     } else {
-        atomicOr(&A.overflow[1], 1u);
+        atomicOr(A.cap_flag, 1u);
         if (bi < A.big_cap) A.big[bi].J = 0u;  // skipped by lc_combine
     }
     const uint64_t arel = prel - g.f;  // the record's first window (chunks j >= 1 start on the grid)
     for (uint32_t j = 0; j < g.J; j++) {
         const bool last = j + 1u == g.J;
         const uint32_t K = last ? g.K - kLCWin * j : kLCWin;
-        lc_put(A, ctr, K, j ? arel + 4096ull * j : prel, j == 0u, last ? g.r : 0u, fits ? kGPart | (pi + j) : kGNull,
-               0u);
+        const uint32_t d = last ? g.r : 0u;
+        const uint32_t rank = atomicAdd(&ctr[lc_bin(K, d)], 1u);
+        lc_desc(A, rs, K, rank, j ? arel + 4096ull * j : prel, j == 0u, d, fits ? kGPart | (pi + j) : kGNull,
+                0u);
     }
 }
 
@@ -224,41 +246,82 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
     A.ev[at] = e;
 }
 
-__global__ __launch_bounds__(kLCWalkThreads) void lc_build_kernel(LCArgs A) {
-    __shared__ uint32_t ctr[kLCCounters];
-    const uint64_t nw = A.n_wg;
-    if (threadIdx.x < kLCCounters)
-        ctr[threadIdx.x] = A.hscan[threadIdx.x * nw + blockIdx.x] - A.hscan[threadIdx.x * nw];
+// A workgroup builds the kLCGroup blocks one walk wave counted (their rank
+// ranges per bin come from the scan): one wave per block at a time, lane j =
+// event j (coalesced slot reads and event writes; the header offsets are the
+// prefix sums of 7 + length over the lanes).
+constexpr uint32_t kLCBuildWaves = 16;
+__device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    uint32_t x = v;
+    for (uint32_t o = 1; o < 64u; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ void lc_finish(const LCArgs &A) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.result[0] = A.start[A.n_blocks];
+        A.result[1] = A.hscan[(uint64_t)kLCCounters * A.n_grp] - A.hscan[(uint64_t)kLCOver * A.n_grp];
+        A.result[2] = *A.cap_flag;
+    }
+}
+
+__global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) {
+    __shared__ uint32_t ctr[kLCCounters], rs[kLCBins];
+    const uint64_t nw = A.n_grp;
+    for (uint32_t i = threadIdx.x; i < kLCCounters; i += blockDim.x)
+        ctr[i] = A.checksum ? A.hscan[i * nw + blockIdx.x] - A.hscan[i * nw] : 0u;
+    for (uint32_t i = threadIdx.x; i < kLCBins && A.checksum; i += blockDim.x) rs[i] = A.rstart[i];
     __syncthreads();
-    const uint64_t b = (uint64_t)blockIdx.x * kLCWalkThreads + threadIdx.x;
-    if (b >= A.n_blocks) return;
-    const uint32_t cnt = A.count[b];
-    const uint64_t st = A.start[b], bs = b * 32768u;
-    const uint32_t kept = cnt < kLCSlots ? cnt : kLCSlots;
-    const uint4 *sl = reinterpret_cast<const uint4 *>(A.slots) + b * kLCSlots;
-    for (uint32_t j = 0; j < kept; j++) {
-        const uint4 s = sl[j];
-        const uint32_t off = s.x & 0xffffu, length = s.x >> 16, type = s.y & 0xffu, kind = (s.y >> 8) & 0xffu;
-        lc_event(A, st + j, bs + off, length, type, kind);
-        if (kind == 1u && A.checksum) lc_place(A, ctr, bs + off + 6u, 1u + length, s.z);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // the wave's blocks wv, wv + 16, ... of the group: all their loads first
+    constexpr uint32_t kPer = kLCGroup / kLCBuildWaves;
+    uint32_t cnt[kPer];
+    uint64_t st[kPer], sl[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++) {
+        const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
+        cnt[i] = b < A.n_blocks ? A.count[b] : 0u;
+        st[i] = b < A.n_blocks ? A.start[b] : 0u;
     }
-    if (cnt <= kLCSlots || !A.exact) return;
-    // exact mode: the events past the slots (a block of many short records) are
-    // walked again from the header after the last kept one (an OK record: only
-    // OK records continue the walk)
-    const uint4 s = sl[kLCSlots - 1u];
-    uint64_t p = bs + (s.x & 0xffffu) + 7u + (s.x >> 16);
-    const uint64_t be = bs + 32768u < A.size ? bs + 32768u : A.size;
-    const bool eof = be - bs < 32768u;
-    for (uint32_t j = kLCSlots; j < cnt; j++) {
-        const uint32_t w = be - p >= 7 ? ld_u32u(A.log + p + 3) : 0u;
-        const uint32_t c = be - p >= 7 ? ld_u32u(A.log + p) : 0u;
-        const LCDecision d = lc_decide(be - p, eof, w);
-        lc_event(A, st + j, p, d.length, d.type, d.kind);
-        if (d.kind == 1u && A.checksum) lc_place(A, ctr, p + 6u, 1u + d.length, c);
-        if (d.stop) break;
-        p += 7u + d.length;
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++) {
+        const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
+        sl[i] = lane < cnt[i] ? A.slots[b * kLCSlots + lane] : 0ull;
     }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++) {
+        const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
+        if (b >= A.n_blocks) break;
+        const uint64_t bs = b * 32768u, s = sl[i];
+        const bool have = lane < cnt[i];  // lane < kLCSlots always
+        const uint32_t length = (uint32_t)s & 0xffffu, type = ((uint32_t)s >> 16) & 0xffu, kind = (uint32_t)s >> 24;
+        const uint32_t stored = (uint32_t)(s >> 32);
+        const uint64_t h = bs + lc_wave_excl_sum(have ? 7u + length : 0u);  // this event's header
+        if (have) lc_event(A, st[i] + lane, h, length, type, kind);
+        if (A.checksum) lc_place(A, ctr, rs, have && kind == 1u, h + 6u, 1u + length, stored);
+        if (cnt[i] <= kLCSlots || !A.exact) continue;
+        // exact mode: the events past the slots (a block of many short records)
+        // are walked again by lane 0 from the header after the last kept one (an
+        // OK record: only OK records continue the walk)
+        uint64_t p = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)h, (int)(kLCSlots - 1u)) |
+                     ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(h >> 32), (int)(kLCSlots - 1u)) << 32);
+        p += 7u + (uint32_t)__builtin_amdgcn_readlane((int)length, (int)(kLCSlots - 1u));
+        const uint64_t be = bs + 32768u < A.size ? bs + 32768u : A.size;
+        const bool eof = be - bs < 32768u;
+        for (uint32_t j = kLCSlots; j < cnt[i]; j++) {
+            const uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
+            const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
+            if (lane == 0u) lc_event(A, st[i] + j, p, d.length, d.type, d.kind);
+            if (A.checksum) lc_place(A, ctr, rs, lane == 0u && d.kind == 1u, p + 6u, 1u + d.length, (uint32_t)hv);
+            if (d.stop) break;
+            p += 7u + d.length;
+        }
+    }
+    if (!A.checksum) lc_finish(A);  // the last kernel of a walk-only verification
 }
 
 // z^L(v) for L < 32768: z^(128 (L >> 7)) then z^(L & 127), 8 nibble lookups each
@@ -274,7 +337,7 @@ __device__ __forceinline__ uint32_t lc_zshift(const uint32_t *aux, uint32_t v, u
 }
 
 __global__ __launch_bounds__(256) void lc_combine_kernel(LCArgs A, uint32_t n_big_max) {
-    const uint64_t nw = A.n_wg;
+    const uint64_t nw = A.n_grp;
     const uint32_t nbig = A.hscan[(kLCBig + 1u) * nw] - A.hscan[kLCBig * nw];
     const uint32_t lim = nbig < n_big_max ? nbig : n_big_max;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
@@ -296,6 +359,7 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t b = t / kLCSlots;
     const uint32_t j = (uint32_t)(t % kLCSlots);
+    lc_finish(A);  // the last kernel: the result words the host reads back
     if (b >= A.n_blocks) return;
     const uint32_t fb = A.first_bad[b];
     if (fb == kLCNone) return;
@@ -311,15 +375,15 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 }
 
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
-    hipLaunchKernelGGL(lc_walk_kernel, dim3(A.n_wg), dim3(kLCWalkThreads), 0, st, A);
+    hipLaunchKernelGGL(lc_walk_kernel, dim3((A.n_grp + 3) / 4), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st) {
-    hipLaunchKernelGGL(lc_setup_kernel, dim3(1), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(lc_setup_kernel, dim3(1), dim3(kLCBins), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_build(const LCArgs &A, hipStream_t st) {
-    hipLaunchKernelGGL(lc_build_kernel, dim3(A.n_wg), dim3(kLCWalkThreads), 0, st, A);
+    hipLaunchKernelGGL(lc_build_kernel, dim3(A.n_grp), dim3(64 * kLCBuildWaves), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st) {
