@@ -165,6 +165,13 @@ constexpr size_t kG4UDword = 38272;
 constexpr size_t kG4T0Dword = 39296;
 constexpr size_t kG4ShiftDword = 36864;  // gv4 image: 7 x 128 dwords (replaces the v4 U4 tables)
 constexpr size_t kG4EDword = 37760;      // gv4 image: 4 x 128 dwords, ends at 38272 = kG4UDword
+// gv4 image: v_perm_b32 byte selectors of a round's first / last step (after T0):
+//   [0, 13)   front, dword starting t = -8..4 bytes from the block start p: byte i
+//             at p + t + i is data (selector i) when >= 0, the seed W's byte
+//             t + i + 4 (selector t + i + 8) when in [-4, 0), else zero (0x0c)
+//   [13, 18)  tail, t' = 0..4 bytes of the dword before the tail pad: byte i kept
+//             (selector i) when i < t', else zero
+constexpr size_t kG4SelDword = 39552;
 inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     const Tables &T = tables();
     const int gap = 16 * lpb - 4;
@@ -209,6 +216,20 @@ inline std::vector<uint32_t> build_lds_image_gv4() {
         for (int p = 0; p < 8; p++)
             for (int v = 0; v < 16; v++)
                 img[kG4EDword + (size_t)e * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), (uint32_t)e);
+    for (int t = -8; t <= 4; t++) {
+        uint32_t sel = 0;
+        for (int i = 0; i < 4; i++) {
+            const int pos = t + i;
+            const uint32_t b = pos >= 0 ? (uint32_t)i : (pos >= -4 ? (uint32_t)(pos + 8) : 0x0cu);
+            sel |= b << (8 * i);
+        }
+        img[kG4SelDword + (size_t)(t + 8)] = sel;
+    }
+    for (int t = 0; t <= 4; t++) {
+        uint32_t sel = 0;
+        for (int i = 0; i < 4; i++) sel |= (i < t ? (uint32_t)i : 0x0cu) << (8 * i);
+        img[kG4SelDword + 13 + (size_t)t] = sel;
+    }
     return img;
 }
 

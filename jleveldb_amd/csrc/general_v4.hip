@@ -422,13 +422,14 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         }
         const uint32_t f = (uint32_t)(cv.p & 127u);
         uint32_t v[4] = {wv.x, wv.y, wv.z, wv.w};
+        // byte selectors from the image (kG4SelByte): v_med3 + one LDS read + v_perm per
+        // dword, no divergent shift code
         if (ce + 1u == cE) {  // last step: zero the tail pad (bytes >= 128 - d of the window)
-            const uint32_t lim = 128u - cv.d;
+            const int tl = (int)(128u - cv.d) - (int)(16u * l);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t u = 16u * l + 4u * j;
-                const uint32_t m = u + 4u <= lim ? 0xffffffffu : (u >= lim ? 0u : 0xffffffffu >> (8u * (u + 4u - lim)));
-                v[j] &= m;
+                const int tt = min(max(tl - 4 * j, 0), 4);
+                v[j] = __builtin_amdgcn_perm(0u, v[j], lds_at(lds, kG4SelByte + 52u + 4u * (uint32_t)tt));
             }
         }
         if (ce == e0) {
@@ -449,11 +450,8 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             if constexpr (GV4<MODE>::LOGC) W = cv.seed ? A.seed0 : 0u;  // record chunks after the first: from 0
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const int t = (int)(16u * l + 4u * j) - (int)f;  // dword start relative to p
-                const uint32_t dmask = t >= 0 ? 0xffffffffu : (t <= -4 ? 0u : 0xffffffffu << (8 * (-t)));
-                const int u = t + 4;  // relative to the seed's first byte
-                const uint32_t sp = (u >= 4 || u <= -4) ? 0u : (u >= 0 ? W >> (8 * u) : W << (8 * (-u)));
-                v[j] = (v[j] & dmask) | sp;
+                const int t = min(max((int)(16u * l + 4u * j) - (int)f, -8), 4);  // dword start relative to p
+                v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, kG4SelByte + 4u * (uint32_t)(t + 8)));
             }
             // virtual dword -4 (chain lane 7 / dword 3 of step -1) when f < 4
             const uint32_t s73 = gstep(lds, f < 4u ? W << (8 * f) : 0u, gl);

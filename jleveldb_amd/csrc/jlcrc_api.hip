@@ -25,6 +25,7 @@ static_assert(jlmath::kLSMaskDword * 4 == jlk::kLSMaskByte && jlmath::kLSStageDw
                   jlmath::kLSLaneDword * 4 == jlk::kLSLaneByte && jlmath::kLSShiftDword * 4 == jlk::kLSShiftByte &&
                   jlmath::kLSEDword * 4 == jlk::kLSEByte,
               "log-stream image layout mismatch");
+static_assert(jlmath::kG4SelDword * 4 == jlk::kG4SelByte, "gv4 image layout mismatch");
 static_assert(jlmath::kAuxZW == 5648 && jlmath::kAuxZB == 5648 + 256 * 128, "aux layout mismatch (log_chunks.hip)");
 static_assert(jlmath::kV4SlotDword == jlk::kV4SlotDword && jlmath::kV4UDword * 4 == jlk::kV4U4Byte, "v4 image layout mismatch");
 

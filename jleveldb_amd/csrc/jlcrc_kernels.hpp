@@ -14,6 +14,7 @@ constexpr uint32_t kG4UByte = 153088;    // general v4: U_j[v] = slice4^-1(v << 
 constexpr uint32_t kG4T0Byte = 157184;   // general v4: T0 (suffix byte step)
 constexpr uint32_t kG4ShiftByte = 147456;  // general v4 image: U_k = z^-(4k), k = 0..6, nibble tables
 constexpr uint32_t kG4EByte = 151040;      // general v4 image: E_e = z^-e, e = 0..3, nibble tables
+constexpr uint32_t kG4SelByte = 158208;    // general v4 image: front / tail byte selectors (crc_math.hpp)
 constexpr uint32_t kGNull = 0xffffffffu; // general v4: empty group of a round
 
 enum : int {
