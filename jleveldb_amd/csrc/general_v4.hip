@@ -681,7 +681,7 @@ hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_
 // ---------------------------------------------------------------------------
 // Round pipeline (a counting sort by K; r1 replaced a 17-bit radix sort plus
 // two scans, ~20 launches, with these three):
-//   hist   per-workgroup LDS histogram of the bins b = min(K, kGSoloKey) of
+//   hist   per-workgroup LDS histogram of the bins b = gv4_key(K, d) of
 //          its chunk of blocks, flushed with one global atomic per non-empty
 //          bin (bins >= kLdsBins count globally); empty blocks get their
 //          result here and take no bin
@@ -713,6 +713,15 @@ __device__ __forceinline__ uint32_t gv4_K(uint64_t p, uint32_t n) {
 }
 
 constexpr uint32_t kLdsBins = 4096;  // bins counted in LDS (K < 4096: blocks < 512 KiB)
+
+// Sort key of a block of K steps with tail pad d: K.  (Keys by (K, d mod 16),
+// which make one round's epilogue tables uniform, cost C3 14 % in r2: a K bin
+// split 16 ways scatters neighbouring arena blocks over far-apart rounds.  The
+// log path bins its chunks that way, log_chunks.hip.)
+__device__ __forceinline__ uint32_t gv4_key(uint32_t K, uint32_t d) {
+    (void)d;
+    return K < kGSoloKey ? K : kGSoloKey;
+}
 
 // Wave-aggregated counting: for every distinct bin among the wave's lanes, one
 // atomic adds the number of lanes in it (to the LDS counter for small bins, the
@@ -758,7 +767,7 @@ __device__ __forceinline__ uint32_t gv4_bin(const KParams &P, uint64_t i, bool w
     gv4_block(P, i, p, n);
     const bool bad = !gv4_in_range(P, i);
     const uint32_t K = bad ? 0u : gv4_K(p, n);
-    if (K) return K < kGSoloKey ? K : kGSoloKey;
+    if (K) return gv4_key(K, (uint32_t)((uint64_t)K * 128u - (p & 127u) - n));
     if (write_empty && bad) {  // a descriptor past the caller's bytes: nothing read, result 0
         if (P.mode == MODE_CRC) P.out32[i] = 0u;
         else P.out8[i] = 0u;
@@ -827,9 +836,10 @@ __global__ __launch_bounds__(1024) void gv4_hist_kernel(KParams P, GSplit S, uin
                     g.m = m;
                     S.big[bid] = g;
                     const GChunks c = gv4_chunks(p, n, cs, m);
-                    if (m > 1u) atomicAdd(&hist[c.kF], m - 1u);
-                    atomicAdd(&hist[c.kL], 1u);
-                    atomicMax(&hist[kGSoloKey + 1u], c.kF > c.kL ? c.kF : c.kL);
+                    const uint32_t bF = gv4_key(c.kF, c.dF), bL = gv4_key(c.kL, c.dL);
+                    if (m > 1u) atomicAdd(&hist[bF], m - 1u);
+                    atomicAdd(&hist[bL], 1u);
+                    atomicMax(&hist[kGSoloKey + 1u], bF > bL ? bF : bL);
                 }
             }
             if (!split) b = gv4_bin(P, i, true);
@@ -958,10 +968,11 @@ __global__ __launch_bounds__(1024) void gv4_place_kernel(KParams P, GSplit S, co
             gv4_split_geom(P, S, n, cs, m);
             const GChunks c = gv4_chunks(p, n, cs, m);
             const uint32_t part0 = S.bigbase[i];
-            const uint32_t rF = m > 1u ? atomicAdd(&cursor[c.kF], m - 1u) : 0u, rL = atomicAdd(&cursor[c.kL], 1u);
+            const uint32_t bF = gv4_key(c.kF, c.dF), bL = gv4_key(c.kL, c.dL);
+            const uint32_t rF = m > 1u ? atomicAdd(&cursor[bF], m - 1u) : 0u, rL = atomicAdd(&cursor[bL], 1u);
             for (uint32_t j = 0; j + 1u < m; j++)
-                gv4_put(desc, rstart, c.kF, rF + j, p + (uint64_t)j * cs, c.dF, kGPart | (part0 + j), c.kF);
-            gv4_put(desc, rstart, c.kL, rL, p + (uint64_t)(m - 1u) * cs, c.dL, kGPart | (part0 + m - 1u), c.kL);
+                gv4_put(desc, rstart, bF, rF + j, p + (uint64_t)j * cs, c.dF, kGPart | (part0 + j), c.kF);
+            gv4_put(desc, rstart, bL, rL, p + (uint64_t)(m - 1u) * cs, c.dL, kGPart | (part0 + m - 1u), c.kL);
             continue;
         }
         const uint32_t r = b < kLdsBins ? base[b] + rank[k] : rank[k];

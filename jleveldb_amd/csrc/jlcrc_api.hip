@@ -217,13 +217,41 @@ int ensure_ready() {
 // ------------------------------------------------------- host input staging
 constexpr uint64_t kRegisterMin = 64ull << 20;  // hipHostRegister only pays for large inputs
 
+// The engine's own call-scoped hipHostRegister pins, shared by reference count:
+// two threads verifying the same mmap'd file at once must not have the first
+// one to finish unpin the range under the other's DMA (hipPointerGetAttributes
+// reports the range as pinned to the second caller, which then copies straight
+// from it).
+struct PinRegistry {
+    std::mutex mu;
+    struct Pin {
+        const void *p;
+        uint64_t bytes;
+        int refs;
+    };
+    std::vector<Pin> pins;
+};
+PinRegistry &pin_registry() {
+    static PinRegistry r;
+    return r;
+}
+
 // A host input range for one call: DMA'd directly when it is pinned
 // (hipHostMalloc'ed or already registered) or could be registered for the call
 // (JL_OPT_HOST_REGISTER), else copied through the slots' pinned staging.
 struct HostSrc {
     const uint8_t *p = nullptr;
-    bool direct = false, registered = false;
-    HostSrc(const void *ptr, uint64_t bytes) : p((const uint8_t *)ptr) {
+    uint64_t bytes = 0;
+    bool direct = false, shared = false;  // shared: holds a reference on an engine pin
+    HostSrc(const void *ptr, uint64_t n) : p((const uint8_t *)ptr), bytes(n) {
+        PinRegistry &R = pin_registry();
+        std::lock_guard<std::mutex> lk(R.mu);
+        for (PinRegistry::Pin &q : R.pins)  // inside a range another call of the engine pinned
+            if ((const uint8_t *)q.p <= p && p + bytes <= (const uint8_t *)q.p + q.bytes) {
+                q.refs++;
+                direct = shared = true;
+                return;
+            }
         hipPointerAttribute_t attr;
         direct = hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeHost;
         (void)hipGetLastError();  // pageable memory reports an error here; clear it
@@ -231,7 +259,8 @@ struct HostSrc {
             // read-only first: an mmap'd file opened O_RDONLY can only be pinned that way
             for (unsigned flags : {(unsigned)hipHostRegisterReadOnly, (unsigned)hipHostRegisterDefault}) {
                 if (hipHostRegister((void *)ptr, bytes, flags) == hipSuccess) {
-                    direct = registered = true;
+                    direct = shared = true;
+                    R.pins.push_back({ptr, bytes, 1});
                     break;
                 }
                 (void)hipGetLastError();  // not registrable (e.g. some file mappings): staging
@@ -239,7 +268,19 @@ struct HostSrc {
         }
     }
     ~HostSrc() {
-        if (registered) (void)hipHostUnregister((void *)p);
+        if (!shared) return;
+        PinRegistry &R = pin_registry();
+        std::lock_guard<std::mutex> lk(R.mu);
+        for (size_t i = 0; i < R.pins.size(); i++) {
+            PinRegistry::Pin &q = R.pins[i];
+            if ((const uint8_t *)q.p <= p && p + bytes <= (const uint8_t *)q.p + q.bytes) {
+                if (--q.refs == 0) {
+                    (void)hipHostUnregister((void *)q.p);
+                    R.pins.erase(R.pins.begin() + (ptrdiff_t)i);
+                }
+                return;
+            }
+        }
     }
 };
 
