@@ -219,7 +219,7 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True, host_copy=Tr
     alg = crc_bytes + 7 * plan["len"].size
     res = {"config": label, "log_bytes": nb, "payload_records": int(lens.size),
            "physical_records": int(plan["len"].size), "records_ok": ok,
-           "path": "walk kernel + batched general v4 crc + finalize (JL_LOG_CHECKSUM)",
+           "path": "header walk + record chunks in exact (K, d) rounds through general v4 + fold/apply (JL_LOG_CHECKSUM)",
            "GiB_per_s": round(nb / (ms / steps / 1e3) / GIB, 1),
            "achieved_GBps": round(alg / (ms / steps / 1e3) / 1e9, 1),
            "ms_per_step": round(ms / steps, 3), "wall_ms_per_step": round(wall / steps * 1e3, 3)}

@@ -216,13 +216,16 @@ typedef struct jl_log_event {
  * to *n_events (host pointer; this call synchronises on the stream).
  * `checksum` (LogReader's checksum flag, J/db/LogReader.java:356):
  *   JL_LOG_NO_CHECKSUM     header walk only, every record accepted;
- *   JL_LOG_CHECKSUM        header walk kernel, then the records' masked crcs as
- *                          one batch through the general v4 kernel (the default);
+ *   JL_LOG_CHECKSUM        header walk kernel, then every OK record's crc range
+ *                          cut into chunks of <= 4 KiB sorted into rounds of one
+ *                          window count through the general v4 kernel (the
+ *                          default; no host round trip before the final event
+ *                          count);
  *   JL_LOG_CHECKSUM_TWO_PASS  the same path (explicit name);
  *   JL_LOG_CHECKSUM_FUSED  one pass over the bytes that walks and verifies
  *                          together (log_stream.hip); same results, slower on
  *                          short records; blocks of more than 256
- *                          records fall back to the two-pass path. */
+ *                          records fall back to the default path. */
 #define JL_LOG_NO_CHECKSUM 0
 #define JL_LOG_CHECKSUM 1
 #define JL_LOG_CHECKSUM_TWO_PASS 2

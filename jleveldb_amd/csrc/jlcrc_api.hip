@@ -538,7 +538,7 @@ static void free_partition(const jlk::KParams &P, uint64_t *part, hipStream_t st
 // run starts -> round ids -> GDesc table), all stream-ordered on `st` with
 // stream-ordered scratch.
 static bool gv4_eligible(const jlk::KParams &P) {
-    if (P.mode != jlk::MODE_CRC && P.mode != jlk::MODE_TABLE_VERIFY && P.mode != jlk::MODE_LOG_VERIFY) return false;
+    if (P.mode != jlk::MODE_CRC && P.mode != jlk::MODE_TABLE_VERIFY) return false;
     if (P.n >= (1ull << 31)) return false;  // hipcub sizes are int
     if (!P.off && (P.fixed_bytes == 0 || P.fixed_bytes > 0xffffffffull)) return false;
     return true;
@@ -551,7 +551,7 @@ static hipError_t gv4_launch(const jlk::GV4Args &A, hipStream_t st) {
     case jlk::MODE_CRC: return jlk::launch_gv4_m<jlk::MODE_CRC>(img, A, ctx().d_zero, grid, st);
     case jlk::MODE_TABLE_VERIFY: return jlk::launch_gv4_m<jlk::MODE_TABLE_VERIFY>(img, A, ctx().d_zero, grid, st);
     case jlk::MODE_LOG_CHUNK: return jlk::launch_gv4_m<jlk::MODE_LOG_CHUNK>(img, A, ctx().d_zero, grid, st);
-    default: return jlk::launch_gv4_m<jlk::MODE_LOG_VERIFY>(img, A, ctx().d_zero, grid, st);
+    default: return hipErrorInvalidValue;
     }
 }
 

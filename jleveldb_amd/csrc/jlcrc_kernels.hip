@@ -1,5 +1,5 @@
 // jlcrc_kernels.hip — CDNA4 (gfx950) kernels of the masked-CRC32C engine:
-// the log walk / finalize / copy kernels, the partition, fill and read-stream
+// the log-writer copy kernel, the partition, fill and read-stream
 // helpers, and — in the study build only (make STUDY=1, -DJL_STUDY=1) — the
 // round-1 kernels the v4 and general-v4 paths superseded, kept for A/B:
 //
@@ -517,107 +517,6 @@ __global__ __launch_bounds__(1024) void crc_general_kernel(const uint4 *__restri
 
 #endif  // JL_STUDY
 
-// ---------------------------------------------------------------------------
-// Log walk (LogReader.readPhysicalRecord header decisions per 32 KiB block,
-// J/db/LogReader.java:297-383).  One thread per block; pass 0 counts events,
-// pass 1 writes them (offsets from an exclusive scan of the counts).  CRC
-// verification of the OK events is done by crc_general_kernel afterwards and
-// applied by log_finalize_kernel.
-// ---------------------------------------------------------------------------
-
-__device__ __forceinline__ void log_put(LogEvent *ev, uint64_t *d_off, uint32_t *d_len, uint64_t at, uint64_t p,
-                                        uint32_t length, uint32_t type, uint8_t kind) {
-    LogEvent e;
-    e.offset = p;
-    e.length = length;
-    e.type = (uint8_t)type;
-    e.kind = kind;
-    e.pad = 0;
-    ev[at] = e;
-    if (kind == 1) { d_off[at] = p + 6; d_len[at] = 1u + length; }
-    else { d_off[at] = p; d_len[at] = 0; }
-}
-
-// With slots (r1): pass 0 also keeps each block's first kLogSlots decisions
-// (8 B each), log_expand_kernel writes them out one thread per event, and pass 1
-// only re-walks the blocks with more events than that.  Without slots pass 1
-// re-walks every block (the walk is a chain of dependent header loads).
-__global__ void log_walk_kernel(const uint8_t *__restrict__ log, uint64_t size, uint64_t n_blocks, int pass,
-                                uint64_t *__restrict__ counts, const uint64_t *__restrict__ starts,
-                                LogEvent *__restrict__ ev, uint64_t *__restrict__ d_off, uint32_t *__restrict__ d_len,
-                                LogSlot *__restrict__ slots) {
-    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= n_blocks) return;
-    if (pass && slots && counts[b] <= kLogSlots) return;  // written by log_expand_kernel
-    const uint64_t bs = b * 32768u;
-    const uint64_t be = (bs + 32768u < size) ? bs + 32768u : size;
-    const bool eof = (be - bs) < 32768u;
-    uint64_t p = bs, cnt = 0;
-    uint64_t o = pass ? starts[b] : 0;
-    // header bytes 3..6 in one unaligned dword load: [crc3][len lo][len hi][type].
-    // The next header's load is issued before this record's slot/event store:
-    // on gfx9 vmcnt counts stores too, so a store issued first would put its
-    // write latency on the walk's serial chain.
-    uint32_t w = (be - p >= 7) ? *(const u32u *)(log + p + 3) : 0u;
-    for (;;) {
-        const uint64_t rem = be - p;
-        uint8_t kind = 0;
-        uint32_t length = 0, type = 0;
-        bool stop = false;
-        if (rem < 7) {
-            if (eof && rem > 0) { kind = 6; stop = true; }
-            else break;
-        } else {
-            length = (w >> 8) & 0xffffu;
-            type = w >> 24;
-            if (7u + (uint64_t)length > rem) { kind = eof ? 5 : 3; stop = true; }
-            else if (type == 0 && length == 0) { kind = 4; stop = true; }
-            else kind = 1;
-        }
-        const uint64_t pn = p + 7u + length;
-        if (!stop && be - pn >= 7) w = *(const u32u *)(log + pn + 3);
-        if (pass) {
-            if (!slots || cnt >= kLogSlots) log_put(ev, d_off, d_len, o + cnt, p, length, type, kind);
-        } else if (slots && cnt < kLogSlots) {
-            // one 8-byte store of the LogSlot {off, length, type, kind, pad} (little endian)
-            static_assert(sizeof(LogSlot) == 8, "LogSlot packs into one dwordx2");
-            reinterpret_cast<uint64_t *>(slots)[b * kLogSlots + cnt] =
-                (uint64_t)(p - bs) | ((uint64_t)length << 16) | ((uint64_t)type << 32) | ((uint64_t)kind << 40);
-        }
-        cnt++;
-        if (stop) break;
-        p = pn;
-    }
-    if (!pass) counts[b] = cnt;
-}
-
-__global__ void log_expand_kernel(uint64_t n_blocks, const uint64_t *__restrict__ counts,
-                                  const uint64_t *__restrict__ starts, const LogSlot *__restrict__ slots,
-                                  LogEvent *__restrict__ ev, uint64_t *__restrict__ d_off, uint32_t *__restrict__ d_len) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t b = t / kLogSlots, j = t % kLogSlots;
-    if (b >= n_blocks || j >= counts[b]) return;
-    const LogSlot sl = slots[t];
-    log_put(ev, d_off, d_len, starts[b] + j, b * 32768u + sl.off, sl.length, sl.type, sl.kind);
-}
-
-// Applies the per-record CRC results (ok[i] = 1 match) and truncates each block
-// after its first mismatch (the reference clears its 32 KiB buffer, :359-367):
-// the failing event becomes BAD_CRC, later events of the block become kind 0
-// (not visible to the reader).
-__global__ void log_finalize_kernel(uint64_t n_blocks, const uint64_t *__restrict__ starts,
-                                    const uint64_t *__restrict__ counts, const uint8_t *__restrict__ ok,
-                                    LogEvent *__restrict__ ev, int checksum) {
-    uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= n_blocks || !checksum) return;
-    const uint64_t s = starts[b], c = counts[b];
-    bool dead = false;
-    for (uint64_t i = s; i < s + c; i++) {
-        if (dead) { ev[i].kind = 0; continue; }
-        if (ev[i].kind == 1 && !ok[i]) { ev[i].kind = 2; dead = true; }
-    }
-}
-
 // Payload copies of a batched LogWriter (jl_log_emit_dev): one workgroup per
 // fragment (grid-stride), byte-granular (arbitrary alignment on both sides);
 // also records each payload's file offset for the header pass.
@@ -775,62 +674,14 @@ hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part
     switch (P.mode) {
     case MODE_CRC: return launch_stream_m<MODE_CRC>(img, P, part, grid, depth, st);
     case MODE_TABLE_VERIFY: return launch_stream_m<MODE_TABLE_VERIFY>(img, P, part, grid, depth, st);
-    case MODE_LOG_VERIFY: return launch_stream_m<MODE_LOG_VERIFY>(img, P, part, grid, depth, st);
     case MODE_TRAILER: return launch_stream_m<MODE_TRAILER>(img, P, part, grid, depth, st);
     case MODE_LOG_HEADER: return launch_stream_m<MODE_LOG_HEADER>(img, P, part, grid, depth, st);
     default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
-                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, LogSlot *slots,
-                           hipStream_t st) {
-    unsigned grid = (unsigned)((n_blocks + 255) / 256);
-    if (pass && slots)
-        hipLaunchKernelGGL(log_expand_kernel, dim3((unsigned)((n_blocks * kLogSlots + 255) / 256)), dim3(256), 0, st,
-                           n_blocks, counts, starts, slots, ev, d_off, d_len);
-    hipLaunchKernelGGL(log_walk_kernel, dim3(grid), dim3(256), 0, st, log, size, n_blocks, pass, counts, starts, ev,
-                       d_off, d_len, slots);
-    return hipGetLastError();
-}
-
 hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, uint64_t *part, hipStream_t st) {
     hipLaunchKernelGGL(partition_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, incl, n, parts, part);
-    return hipGetLastError();
-}
-
-// Event-parallel form of log_finalize_kernel (r1: one thread per 32 KiB block
-// walked its events serially): the first failing OK event of each block by an
-// atomicMin, then every event of the block compares its index with it.
-__global__ void log_firstbad_kernel(uint64_t n_events, const uint8_t *__restrict__ ok, const LogEvent *__restrict__ ev,
-                                    unsigned long long *__restrict__ firstbad) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_events) return;
-    if (ev[i].kind == 1 && !ok[i]) atomicMin(&firstbad[ev[i].offset / 32768u], (unsigned long long)i);
-}
-__global__ void log_apply_kernel(uint64_t n_events, const unsigned long long *__restrict__ firstbad,
-                                 LogEvent *__restrict__ ev) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_events) return;
-    const unsigned long long fb = firstbad[ev[i].offset / 32768u];
-    if (i == fb) ev[i].kind = 2;
-    else if (i > fb) ev[i].kind = 0;
-}
-
-hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
-                               LogEvent *ev, int checksum, uint64_t n_events, unsigned long long *firstbad,
-                               hipStream_t st) {
-    if (firstbad) {  // event-parallel (firstbad: n_blocks words of scratch)
-        if (!checksum || n_events == 0) return hipSuccess;
-        hipError_t e = hipMemsetAsync(firstbad, 0xff, n_blocks * sizeof(unsigned long long), st);
-        if (e != hipSuccess) return e;
-        const unsigned g = (unsigned)((n_events + 255) / 256);
-        hipLaunchKernelGGL(log_firstbad_kernel, dim3(g), dim3(256), 0, st, n_events, ok, ev, firstbad);
-        hipLaunchKernelGGL(log_apply_kernel, dim3(g), dim3(256), 0, st, n_events, firstbad, ev);
-        return hipGetLastError();
-    }
-    unsigned grid = (unsigned)((n_blocks + 255) / 256);
-    hipLaunchKernelGGL(log_finalize_kernel, dim3(grid), dim3(256), 0, st, n_blocks, starts, counts, ok, ev, checksum);
     return hipGetLastError();
 }
 

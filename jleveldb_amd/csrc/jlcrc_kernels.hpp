@@ -175,7 +175,7 @@ hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *z
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
                              int grid, int lpb, int nt, int shape, hipStream_t st);
 hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
-// general v4 main kernel, one specialisation per mode (general_v4.hip -DJL_MODE=k; modes 0-2)
+// general v4 main kernel, one specialisation per mode (general_v4.hip -DJL_MODE=k; modes 0, 1, 5)
 template <int MODE>
 hipError_t launch_gv4_m(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st);
 // sorted-pipeline helpers (general_v4.hip, mode-0 object)
@@ -187,29 +187,10 @@ hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part
 // one specialisation per mode, each in its own object (stream_kernel.hip -DJL_MODE=k)
 template <int MODE>
 hipError_t launch_stream_m(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st);
-// log walk: pass 0 counts events per 32 KiB block (and keeps the first kLogSlots
-// decisions of each in `slots` when given), pass 1 writes them (slots: expand +
-// re-walk of the blocks with more events)
-constexpr uint64_t kLogSlots = 64;
-struct LogSlot {
-    uint16_t off;     // header offset in the block
-    uint16_t length;
-    uint8_t type, kind;
-    uint16_t pad;
-};
-hipError_t launch_log_walk(const uint8_t *log, uint64_t size, uint64_t n_blocks, int pass, uint64_t *counts,
-                           const uint64_t *starts, LogEvent *ev, uint64_t *d_off, uint32_t *d_len, LogSlot *slots,
-                           hipStream_t st);
 // Byte-balanced partition of n blocks over `parts` waves for the stream kernel:
 // incl[i] = sum of weights of blocks 0..i (weight = len + per-block overhead);
 // part[w] = first block of wave w (part[0] = 0, part[parts] = n).
 hipError_t launch_partition(const uint64_t *incl, uint64_t n, uint64_t parts, uint64_t *part, hipStream_t st);
-// applies the CRC results to the events (BAD_CRC at a block's first failure,
-// its later events hidden); firstbad (n_blocks words of scratch) selects the
-// event-parallel form, null the block-serial one
-hipError_t launch_log_finalize(uint64_t n_blocks, const uint64_t *starts, const uint64_t *counts, const uint8_t *ok,
-                               LogEvent *ev, int checksum, uint64_t n_events, unsigned long long *firstbad,
-                               hipStream_t st);
 // Fused log verification (log_stream.hip): one pass over the log, 8 lanes per
 // 32 KiB block and 8 blocks per wave; walks the headers from the streamed bytes
 // and folds every record's crc.  Per block: the events it walked (up to `cap`

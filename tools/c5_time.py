@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Times config C5 (device-resident WAL verification, both payload sets) through
-the fused and the two-pass log paths — bench.py's secondary_c5 without the CPU
+the fused and the default (walk + chunked rounds) log paths — bench.py's secondary_c5 without the CPU
 leg.  Usage: python tools/c5_time.py [steps] [sets: both | c1 | mixed] [device: skip the copy-inclusive leg]"""
 import json
 import os
