@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
+#include <algorithm>
 #include <utility>
 #include <vector>
 
@@ -230,6 +231,14 @@ inline std::vector<uint32_t> build_lds_image_gv4() {
         for (int i = 0; i < 4; i++) sel |= (i < t ? (uint32_t)i : 0x0cu) << (8 * i);
         img[kG4SelDword + 13 + (size_t)t] = sel;
     }
+    return img;
+}
+// The gv4 kernel's image: build_lds_image_gv4() rotated so region B comes first
+// (byte 0) and the G tables follow at byte 32768 (general_v4.hip kGOff): region-B
+// table bases then fit the ds_read immediate offset.
+inline std::vector<uint32_t> build_lds_image_gv4_rotated() {
+    std::vector<uint32_t> img = build_lds_image_gv4();
+    std::rotate(img.begin(), img.begin() + 32768, img.end());
     return img;
 }
 

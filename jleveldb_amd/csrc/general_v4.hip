@@ -56,6 +56,15 @@ namespace jlk {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
+// The gv4 image is the general v4 image ROTATED (crc_math.hpp
+// build_lds_image_gv4): region B (epilogue tables) at byte 0, the G tables at
+// kGOff.  Every region-B table base is then below 64 KiB and folds into the
+// ds_read immediate offset (an epilogue nibble lookup costs 2 VALU instead of
+// 3), and the G lookups reach their tables through the immediate kGOff.
+constexpr uint32_t kGOff = 32768, kRB = 131072;  // G tables; region B of the unrotated image
+constexpr uint32_t kLaneB = 0, kShiftB = kG4ShiftByte - kRB, kEB = kG4EByte - kRB, kUB = kG4UByte - kRB,
+                   kT0B = kG4T0Byte - kRB, kSelB = kG4SelByte - kRB;
+
 // The pinned registers: two round-descriptor sets (JL_GV4_DQ0/1) and the 8
 // ring slots (slot, register quad, its 4 registers), the top 40 VGPRs a wave of
 // this shape may use: v88..v127 at 16 waves per CU (1024 threads, 128 VGPRs),
@@ -366,6 +375,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     constexpr bool DBG = VAR == 4;  // JL_GV4_DEBUG builds the address checks in
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
+    const uint32_t *ldsG = lds + kGOff / 4u;  // the G tables (rotated image)
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
     const GLanes gl(lane);
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
@@ -429,7 +439,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int tt = min(max(tl - 4 * j, 0), 4);
-                v[j] = __builtin_amdgcn_perm(0u, v[j], lds_at(lds, kG4SelByte + 52u + 4u * (uint32_t)tt));
+                v[j] = __builtin_amdgcn_perm(0u, v[j], lds_at(lds, kSelB + 52u + 4u * (uint32_t)tt));
             }
         }
         if (ce == e0) {
@@ -442,29 +452,28 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                 const uint32_t k = (uint32_t)(ia >> 2) & 3u;
                 const uint32_t own = k & 2u ? (k & 1u ? side_c.w : side_c.z) : (k & 1u ? side_c.y : side_c.x);
                 const uint32_t y = ~(uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane & ~7u) << 2), (int)own);
-                W = lds_at(lds, kG4UByte + ((y & 0xffu) << 2)) ^ lds_at(lds, kG4UByte + 1024u + (((y >> 8) & 0xffu) << 2)) ^
-                    lds_at(lds, kG4UByte + 2048u + (((y >> 16) & 0xffu) << 2)) ^
-                    lds_at(lds, kG4UByte + 3072u + ((y >> 24) << 2));
+                W = lds_at(lds, kUB + ((y & 0xffu) << 2)) ^ lds_at(lds, kUB + 1024u + (((y >> 8) & 0xffu) << 2)) ^
+                    lds_at(lds, kUB + 2048u + (((y >> 16) & 0xffu) << 2)) ^ lds_at(lds, kUB + 3072u + ((y >> 24) << 2));
             }
             if (MODE == MODE_CRC && cv.idx >= kGPart) W = 0u;  // chunk of a split block: from state 0
             if constexpr (GV4<MODE>::LOGC) W = cv.seed ? A.seed0 : 0u;  // record chunks after the first: from 0
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int t = min(max((int)(16u * l + 4u * j) - (int)f, -8), 4);  // dword start relative to p
-                v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, kG4SelByte + 4u * (uint32_t)(t + 8)));
+                v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, kSelB + 4u * (uint32_t)(t + 8)));
             }
             // virtual dword -4 (chain lane 7 / dword 3 of step -1) when f < 4
-            const uint32_t s73 = gstep(lds, f < 4u ? W << (8 * f) : 0u, gl);
+            const uint32_t s73 = gstep(ldsG, f < 4u ? W << (8 * f) : 0u, gl);
             const uint32_t i73 = (l == 7u && f < 4u) ? s73 : zero_v;
             x0 = zero_v ^ v[0];
             x1 = zero_v ^ v[1];
             x2 = zero_v ^ v[2];
             x3 = i73 ^ v[3];
         } else {
-            x0 = gstep_x3(lds, x0, gl, v[0]);
-            x1 = gstep_x3(lds, x1, gl, v[1]);
-            x2 = gstep_x3(lds, x2, gl, v[2]);
-            x3 = gstep_x3(lds, x3, gl, v[3]);
+            x0 = gstep_x3(ldsG, x0, gl, v[0]);
+            x1 = gstep_x3(ldsG, x1, gl, v[1]);
+            x2 = gstep_x3(ldsG, x2, gl, v[2]);
+            x3 = gstep_x3(ldsG, x3, gl, v[3]);
         }
     };
     // end of a round: epilogue, result, next round of the compute cursor; false when done
@@ -473,14 +482,14 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         // = 16 a + 4 c + e bytes past the block: shift by z^-(4 (j + c)), then by
         // z^-(16 (l + a)) (lane tables), group xor, then z^-e
         const uint32_t d = cv.d, sa = 512u * ((d >> 2) & 3u);
-        const uint32_t s0 = gstep_x3(lds, x0, gl, 0u), s1 = gstep_x3(lds, x1, gl, 0u);
-        const uint32_t s2 = gstep_x3(lds, x2, gl, 0u), s3 = gstep_x3(lds, x3, gl, 0u);
-        const uint32_t c = xor3(ushift(lds, s0, kG4ShiftByte + sa), ushift(lds, s1, kG4ShiftByte + 512u + sa),
-                                ushift(lds, s2, kG4ShiftByte + 1024u + sa)) ^
-                           ushift(lds, s3, kG4ShiftByte + 1536u + sa);
+        const uint32_t s0 = gstep_x3(ldsG, x0, gl, 0u), s1 = gstep_x3(ldsG, x1, gl, 0u);
+        const uint32_t s2 = gstep_x3(ldsG, x2, gl, 0u), s3 = gstep_x3(ldsG, x3, gl, 0u);
+        const uint32_t c = xor3(ushift(lds, s0, kShiftB + sa), ushift(lds, s1, kShiftB + 512u + sa),
+                                ushift(lds, s2, kShiftB + 1024u + sa)) ^
+                           ushift(lds, s3, kShiftB + 1536u + sa);
         const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
-        uint32_t st = group_xor<8>(realign(lds, c, 131072u | (col << 2)));
-        st = ushift(lds, st, kG4EByte + 512u * (d & 3u));
+        uint32_t st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
+        st = ushift(lds, st, kEB + 512u * (d & 3u));
         // side chunks of lanes 0 and 1 of the group, seen from lane 0 (DPP row_shl:1)
         const uint32_t h0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.x, 0x101, 0xf, 0xf, false);
         const uint32_t h1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.y, 0x101, 0xf, 0xf, false);
@@ -493,7 +502,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             const uint32_t k = (uint32_t)(sa >> 2) & 3u;
             const uint32_t dw = k & 2u ? (k & 1u ? h3 : h2) : (k & 1u ? h1 : h0);
             const uint32_t sfx = (dw >> (8u * (uint32_t)(sa & 3u))) & 0xffu;
-            st = (st >> 8) ^ lds_at(lds, kG4T0Byte + (((st ^ sfx) & 0xffu) << 2));
+            st = (st >> 8) ^ lds_at(lds, kT0B + (((st ^ sfx) & 0xffu) << 2));
         }
         const uint32_t crc = ~st, m = mask_crc(crc);
         if (DBG && A.P.dbg && l == 0u && cv.idx < kGPart && cv.idx >= A.P.n) {
@@ -558,9 +567,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     // orders memory operations around it, so one per chain would serialise the
     // chains' LDS latencies)
 #define JL_LK(x, T, A3)                                                                                    \
-    const uint32_t T = xor3(lds_at(lds, JL_GADDR(gl.l3, x, 0u)), lds_at(lds, JL_GADDR(gl.l2, x, 1u)),      \
-                            lds_at(lds, JL_GADDR(gl.l1, x, 2u)));                                          \
-    const uint32_t A3 = lds_at(lds, JL_GADDR(gl.l0, x, 3u));
+    const uint32_t T = xor3(lds_at(ldsG, JL_GADDR(gl.l3, x, 0u)), lds_at(ldsG, JL_GADDR(gl.l2, x, 1u)),    \
+                            lds_at(ldsG, JL_GADDR(gl.l1, x, 2u)));                                         \
+    const uint32_t A3 = lds_at(ldsG, JL_GADDR(gl.l0, x, 3u));
 #define JL_XS4(R0, R1, R2, R3)                                                                             \
     {                                                                                                      \
         JL_LK(x0, t0_, u0_) JL_LK(x1, t1_, u1_) JL_LK(x2, t2_, u2_) JL_LK(x3, t3_, u3_)                    \

@@ -795,7 +795,7 @@ int jl_init(int device) {
     JL_HIP(hipMalloc((void **)&c.d_scratch, 4096));
     JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     for (int i = 0; i < 4; i++) {
-        std::vector<uint32_t> v4 = i < 3 ? jlmath::build_lds_image_v4(4 << i) : jlmath::build_lds_image_gv4();
+        std::vector<uint32_t> v4 = i < 3 ? jlmath::build_lds_image_v4(4 << i) : jlmath::build_lds_image_gv4_rotated();
         JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
         JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     }
