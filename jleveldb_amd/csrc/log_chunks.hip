@@ -90,8 +90,16 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
 // Walk groups of kLCGroup consecutive blocks, one per wave (4 per workgroup).
 // The walk also initialises what later kernels accumulate into (first_bad,
 // count[n_blocks], the scan's zero tail, cap_flag): no memsets.
+//
+// Latency: a block's headers form a chain of dependent loads, so the walk is
+// one DRAM round trip per record.  The first kLCLdsSlots events of a block are
+// buffered in LDS and written out after the walk: a global store in the loop
+// makes every hop also wait for the store's acknowledgement (gfx9 counts stores
+// in vmcnt, and the compiler waits vmcnt(0) with a store outstanding).
+constexpr uint32_t kLCLdsSlots = 34;
 __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     __shared__ uint32_t h[4][kLCCounters];
+    __shared__ uint64_t ls[kLCLdsSlots][256];  // [slot][thread]: conflict-free writes
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) (&h[0][0])[i] = 0;
     __syncthreads();
@@ -101,16 +109,13 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         A.hist[(uint64_t)kLCCounters * A.n_grp] = 0;
         *A.cap_flag = 0;
     }
+    uint32_t cnt = 0;
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
         const uint64_t bs = b * 32768u, be = bs + 32768u < A.size ? bs + 32768u : A.size;
         const bool eof = be - bs < 32768u;
         const uint64_t base = (uint64_t)(uintptr_t)A.log;
         uint64_t p = bs;
-        uint32_t cnt = 0;
-        // the next header's load is issued before this record's slot store:
-        // vmcnt counts stores too on gfx9, and a store issued first would put
-        // its latency on the walk's serial chain
         uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
         for (;;) {
             const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
@@ -118,12 +123,13 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
             const uint64_t pn = p + 7u + d.length;
             const uint32_t stored = (uint32_t)hv;
             if (!d.stop && be - pn >= 7) hv = lc_header(A.log + pn, be - pn);
-            const bool kept = cnt < kLCSlots;
-            if (kept) A.slots[b * kLCSlots + cnt] = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
+            const uint64_t slot = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
+            if (cnt < kLCLdsSlots) ls[cnt][threadIdx.x] = slot;
+            else if (cnt < kLCSlots) A.slots[b * kLCSlots + cnt] = slot;
             // chunk histogram: exactly the chunks lc_build places (in the fast
             // mode only the kept events: a block that overflows its slots makes
             // the caller run the exact mode)
-            if (d.kind == 1u && A.checksum && (kept || A.exact)) {
+            if (d.kind == 1u && A.checksum && (cnt < kLCSlots || A.exact)) {
                 const LCGeom g = lc_geom(base + p + 6u, 1u + d.length);
                 if (g.J == 1u) {
                     atomicAdd(&h[wv][lc_bin(g.K, g.r)], 1u);
@@ -142,6 +148,9 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         if (cnt > kLCSlots) atomicAdd(&h[wv][kLCOver], 1u);
     }
     __syncthreads();
+    // the LDS slots out: slot j of the workgroup's 256 blocks
+    const uint32_t kept = cnt < kLCLdsSlots ? cnt : kLCLdsSlots;
+    for (uint32_t j = 0; j < kept; j++) A.slots[b * kLCSlots + j] = ls[j][threadIdx.x];
     const uint64_t g0 = (uint64_t)blockIdx.x * 4u;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) {
         const uint32_t g = i % 4u, c = i / 4u;  // 4 consecutive groups of one counter: one 16-B run
