@@ -241,6 +241,27 @@ inline std::vector<uint32_t> build_lds_image_gv4_rotated() {
     std::rotate(img.begin(), img.begin() + 32768, img.end());
     return img;
 }
+// The log-chunk kernel's image (crc_gv4_kernel<MODE_LOG_CHUNK>): the rotated gv4
+// image with its region B re-cut after the lane tables.  A round's chunks share
+// d mod 16 (bins by (K, d mod 16), log_chunks.hip), so the tail pad's z^-e joins
+// the chain shifts: chain j uses M_m = z^-m, m = 4 (j + c) + e (28 nibble tables)
+// and the epilogue has no separate z^-e stage.  No init / suffix tables (log
+// records are crc'd from value()'s init with no suffix).
+//   byte [16384, 30720)  M_m, m = 0..27, 128 dwords each
+//   byte [30720, 30792)  the front / tail byte selectors (kG4SelDword layout)
+constexpr size_t kLCMDword = 4096, kLCSelDword = 7680;
+inline std::vector<uint32_t> build_lds_image_logchunk() {
+    const Tables &T = tables();
+    std::vector<uint32_t> img = build_lds_image_gv4_rotated();
+    const std::vector<uint32_t> base = build_lds_image_gv4();
+    for (size_t i = kLCMDword; i < 8192; i++) img[i] = 0;
+    for (int m = 0; m < 28; m++)
+        for (int p = 0; p < 8; p++)
+            for (int v = 0; v < 16; v++)
+                img[kLCMDword + (size_t)m * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), (uint32_t)m);
+    for (int i = 0; i < 18; i++) img[kLCSelDword + i] = base[kG4SelDword + i];
+    return img;
+}
 
 // Log-stream image (log_stream.hip): region A = the general v4 gap tables
 // (z^(124+t)∘T0, chains 128 B apart); region B re-cut for the fused log kernel

@@ -64,6 +64,9 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 constexpr uint32_t kGOff = 32768, kRB = 131072;  // G tables; region B of the unrotated image
 constexpr uint32_t kLaneB = 0, kShiftB = kG4ShiftByte - kRB, kEB = kG4EByte - kRB, kUB = kG4UByte - kRB,
                    kT0B = kG4T0Byte - kRB, kSelB = kG4SelByte - kRB;
+// MODE_LOG_CHUNK's image (crc_math.hpp build_lds_image_logchunk): chain tables
+// z^-(4 (j + c) + e) and the byte selectors after the lane tables
+constexpr uint32_t kLCMB = 16384, kLCSelB = 30720;
 
 // The pinned registers: two round-descriptor sets (JL_GV4_DQ0/1) and the 8
 // ring slots (slot, register quad, its 4 registers), the top 40 VGPRs a wave of
@@ -439,7 +442,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int tt = min(max(tl - 4 * j, 0), 4);
-                v[j] = __builtin_amdgcn_perm(0u, v[j], lds_at(lds, kSelB + 52u + 4u * (uint32_t)tt));
+                v[j] = __builtin_amdgcn_perm(0u, v[j], lds_at(lds, (GV4<MODE>::LOGC ? kLCSelB : kSelB) + 52u + 4u * (uint32_t)tt));
             }
         }
         if (ce == e0) {
@@ -460,7 +463,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const int t = min(max((int)(16u * l + 4u * j) - (int)f, -8), 4);  // dword start relative to p
-                v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, kSelB + 4u * (uint32_t)(t + 8)));
+                v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, (GV4<MODE>::LOGC ? kLCSelB : kSelB) + 4u * (uint32_t)(t + 8)));
             }
             // virtual dword -4 (chain lane 7 / dword 3 of step -1) when f < 4
             const uint32_t s73 = gstep(ldsG, f < 4u ? W << (8 * f) : 0u, gl);
@@ -481,15 +484,24 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         // chain (l, j) ends at 16 l + 4 j past the last window, the window ends d
         // = 16 a + 4 c + e bytes past the block: shift by z^-(4 (j + c)), then by
         // z^-(16 (l + a)) (lane tables), group xor, then z^-e
-        const uint32_t d = cv.d, sa = 512u * ((d >> 2) & 3u);
+        const uint32_t d = cv.d;
         const uint32_t s0 = gstep_x3(ldsG, x0, gl, 0u), s1 = gstep_x3(ldsG, x1, gl, 0u);
         const uint32_t s2 = gstep_x3(ldsG, x2, gl, 0u), s3 = gstep_x3(ldsG, x3, gl, 0u);
-        const uint32_t c = xor3(ushift(lds, s0, kShiftB + sa), ushift(lds, s1, kShiftB + 512u + sa),
-                                ushift(lds, s2, kShiftB + 1024u + sa)) ^
-                           ushift(lds, s3, kShiftB + 1536u + sa);
         const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
-        uint32_t st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
-        st = ushift(lds, st, kEB + 512u * (d & 3u));
+        uint32_t st;
+        if constexpr (GV4<MODE>::LOGC) {  // chain j: z^-(4 (j + c) + e) in one table (uniform d mod 16)
+            const uint32_t sm = kLCMB + 512u * (d & 15u);
+            const uint32_t c = xor3(ushift(lds, s0, sm), ushift(lds, s1, sm + 2048u), ushift(lds, s2, sm + 4096u)) ^
+                               ushift(lds, s3, sm + 6144u);
+            st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
+        } else {
+            const uint32_t sa = 512u * ((d >> 2) & 3u);
+            const uint32_t c = xor3(ushift(lds, s0, kShiftB + sa), ushift(lds, s1, kShiftB + 512u + sa),
+                                    ushift(lds, s2, kShiftB + 1024u + sa)) ^
+                               ushift(lds, s3, kShiftB + 1536u + sa);
+            st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
+            st = ushift(lds, st, kEB + 512u * (d & 3u));
+        }
         // side chunks of lanes 0 and 1 of the group, seen from lane 0 (DPP row_shl:1)
         const uint32_t h0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.x, 0x101, 0xf, 0xf, false);
         const uint32_t h1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)side_c.y, 0x101, 0xf, 0xf, false);

@@ -25,7 +25,8 @@ static_assert(jlmath::kLSMaskDword * 4 == jlk::kLSMaskByte && jlmath::kLSStageDw
                   jlmath::kLSLaneDword * 4 == jlk::kLSLaneByte && jlmath::kLSShiftDword * 4 == jlk::kLSShiftByte &&
                   jlmath::kLSEDword * 4 == jlk::kLSEByte,
               "log-stream image layout mismatch");
-static_assert(jlmath::kG4SelDword * 4 == jlk::kG4SelByte, "gv4 image layout mismatch");
+static_assert(jlmath::kG4SelDword * 4 == jlk::kG4SelByte && jlmath::kLCMDword * 4 == 16384 && jlmath::kLCSelDword * 4 == 30720,
+              "gv4 image layout mismatch");
 static_assert(jlmath::kAuxZW == 5648 && jlmath::kAuxZB == 5648 + 256 * 128, "aux layout mismatch (log_chunks.hip)");
 static_assert(jlmath::kV4SlotDword == jlk::kV4SlotDword && jlmath::kV4UDword * 4 == jlk::kV4U4Byte, "v4 image layout mismatch");
 
@@ -135,7 +136,7 @@ struct Context {
     int gen = 0;  // bumped by every jl_init: threads re-bind their HIP device
     int cus = 0;
     void *d_img = nullptr;   // 160 KiB LDS image
-    void *d_img_v4[4] = {nullptr, nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block; [3] gv4
+    void *d_img_v4[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // v4 images for 4 / 8 / 16 lanes per block; [3] gv4; [4] gv4 log chunks
     void *d_img_log = nullptr;  // fused log-verify image (log_stream.hip)
     uint32_t *d_aux = nullptr;
     uint8_t *d_zero = nullptr;  // 4 KiB of zeros (read by predicated-off loads)
@@ -550,7 +551,7 @@ static hipError_t gv4_launch(const jlk::GV4Args &A, hipStream_t st) {
     switch (A.P.mode) {
     case jlk::MODE_CRC: return jlk::launch_gv4_m<jlk::MODE_CRC>(img, A, ctx().d_zero, grid, st);
     case jlk::MODE_TABLE_VERIFY: return jlk::launch_gv4_m<jlk::MODE_TABLE_VERIFY>(img, A, ctx().d_zero, grid, st);
-    case jlk::MODE_LOG_CHUNK: return jlk::launch_gv4_m<jlk::MODE_LOG_CHUNK>(img, A, ctx().d_zero, grid, st);
+    case jlk::MODE_LOG_CHUNK: return jlk::launch_gv4_m<jlk::MODE_LOG_CHUNK>(ctx().d_img_v4[4], A, ctx().d_zero, grid, st);
     default: return hipErrorInvalidValue;
     }
 }
@@ -794,8 +795,10 @@ int jl_init(int device) {
     JL_HIP(hipMalloc((void **)&c.d_zero, 4096));
     JL_HIP(hipMalloc((void **)&c.d_scratch, 4096));
     JL_HIP(hipMemcpy(c.d_img, img.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
-    for (int i = 0; i < 4; i++) {
-        std::vector<uint32_t> v4 = i < 3 ? jlmath::build_lds_image_v4(4 << i) : jlmath::build_lds_image_gv4_rotated();
+    for (int i = 0; i < 5; i++) {
+        std::vector<uint32_t> v4 = i < 3    ? jlmath::build_lds_image_v4(4 << i)
+                                   : i == 3 ? jlmath::build_lds_image_gv4_rotated()
+                                            : jlmath::build_lds_image_logchunk();
         JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
         JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     }

@@ -259,7 +259,7 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
 // ranges per bin come from the scan): one wave per block at a time, lane j =
 // event j (coalesced slot reads and event writes; the header offsets are the
 // prefix sums of 7 + length over the lanes).
-constexpr uint32_t kLCBuildWaves = 16;
+constexpr uint32_t kLCBuildWaves = 4;  // 16 blocks per wave, all their loads issued first: one occupancy batch
 __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
     const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     uint32_t x = v;
