@@ -244,12 +244,22 @@ inline std::vector<uint32_t> build_lds_image_gv4_rotated() {
 // The log-chunk kernel's image (crc_gv4_kernel<MODE_LOG_CHUNK>): the rotated gv4
 // image with its region B re-cut after the lane tables.  A round's chunks share
 // d mod 16 (bins by (K, d mod 16), log_chunks.hip), so the tail pad's z^-e joins
-// the chain shifts: chain j uses M_m = z^-m, m = 4 (j + c) + e (28 nibble tables)
-// and the epilogue has no separate z^-e stage.  No init / suffix tables (log
-// records are crc'd from value()'s init with no suffix).
+// the chain shifts: chain j uses M_m, m = 4 (j + c) + e (28 nibble tables) and
+// the epilogue has no separate z^-e stage.  The tables also absorb the chains'
+// last pending step: after a round's last window a chain register x still owes
+// its lookups, the 8-lane gap step L(x) = G3[x.b0] ^ G2[x.b1] ^ G1[x.b2] ^
+// G0[x.b3] (G_t = z^(124+t)∘T0, linear), so M_m = z^-m ∘ L is applied to the
+// chain registers directly (16 G lookups per round less).  No init / suffix
+// tables (log records are crc'd from value()'s init with no suffix).
 //   byte [16384, 30720)  M_m, m = 0..27, 128 dwords each
 //   byte [30720, 30792)  the front / tail byte selectors (kG4SelDword layout)
 constexpr size_t kLCMDword = 4096, kLCSelDword = 7680;
+inline uint32_t gap_step8(uint32_t x) {  // L above (8 lanes per block: gap 124)
+    const Tables &T = tables();
+    uint32_t r = 0;
+    for (int t = 0; t < 4; t++) r ^= T.zn(T.t[0][(x >> (8 * t)) & 0xffu], 124u + 3u - (uint32_t)t);
+    return r;
+}
 inline std::vector<uint32_t> build_lds_image_logchunk() {
     const Tables &T = tables();
     std::vector<uint32_t> img = build_lds_image_gv4_rotated();
@@ -258,7 +268,7 @@ inline std::vector<uint32_t> build_lds_image_logchunk() {
     for (int m = 0; m < 28; m++)
         for (int p = 0; p < 8; p++)
             for (int v = 0; v < 16; v++)
-                img[kLCMDword + (size_t)m * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), (uint32_t)m);
+                img[kLCMDword + (size_t)m * 128 + p * 16 + v] = T.zinvn(gap_step8((uint32_t)v << (4 * p)), (uint32_t)m);
     for (int i = 0; i < 18; i++) img[kLCSelDword + i] = base[kG4SelDword + i];
     return img;
 }

@@ -466,8 +466,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                 v[j] = __builtin_amdgcn_perm(W, v[j], lds_at(lds, (GV4<MODE>::LOGC ? kLCSelB : kSelB) + 4u * (uint32_t)(t + 8)));
             }
             // virtual dword -4 (chain lane 7 / dword 3 of step -1) when f < 4
-            const uint32_t s73 = gstep(ldsG, f < 4u ? W << (8 * f) : 0u, gl);
-            const uint32_t i73 = (l == 7u && f < 4u) ? s73 : zero_v;
+            // (a divergent branch: most rounds have no such lane and skip it)
+            uint32_t i73 = zero_v;
+            if (l == 7u && f < 4u) i73 = gstep(ldsG, W << (8 * f), gl);
             x0 = zero_v ^ v[0];
             x1 = zero_v ^ v[1];
             x2 = zero_v ^ v[2];
@@ -485,16 +486,18 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         // = 16 a + 4 c + e bytes past the block: shift by z^-(4 (j + c)), then by
         // z^-(16 (l + a)) (lane tables), group xor, then z^-e
         const uint32_t d = cv.d;
-        const uint32_t s0 = gstep_x3(ldsG, x0, gl, 0u), s1 = gstep_x3(ldsG, x1, gl, 0u);
-        const uint32_t s2 = gstep_x3(ldsG, x2, gl, 0u), s3 = gstep_x3(ldsG, x3, gl, 0u);
         const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
         uint32_t st;
-        if constexpr (GV4<MODE>::LOGC) {  // chain j: z^-(4 (j + c) + e) in one table (uniform d mod 16)
+        if constexpr (GV4<MODE>::LOGC) {
+            // chain j: its pending gap step, then z^-(4 (j + c) + e), in one table
+            // (uniform d mod 16; crc_math.hpp build_lds_image_logchunk)
             const uint32_t sm = kLCMB + 512u * (d & 15u);
-            const uint32_t c = xor3(ushift(lds, s0, sm), ushift(lds, s1, sm + 2048u), ushift(lds, s2, sm + 4096u)) ^
-                               ushift(lds, s3, sm + 6144u);
+            const uint32_t c = xor3(ushift(lds, x0, sm), ushift(lds, x1, sm + 2048u), ushift(lds, x2, sm + 4096u)) ^
+                               ushift(lds, x3, sm + 6144u);
             st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
         } else {
+            const uint32_t s0 = gstep_x3(ldsG, x0, gl, 0u), s1 = gstep_x3(ldsG, x1, gl, 0u);
+            const uint32_t s2 = gstep_x3(ldsG, x2, gl, 0u), s3 = gstep_x3(ldsG, x3, gl, 0u);
             const uint32_t sa = 512u * ((d >> 2) & 3u);
             const uint32_t c = xor3(ushift(lds, s0, kShiftB + sa), ushift(lds, s1, kShiftB + 512u + sa),
                                     ushift(lds, s2, kShiftB + 1024u + sa)) ^

@@ -15,7 +15,9 @@
   both payload sets (1 056-B C1-shaped records; mixed 1 B - 100 KiB records that
   fragment FIRST/MIDDLE/LAST), verified device-resident (jl_log_verify_dev) and
   compared event-for-event with the oracle's readPhysicalRecord walk
-  (J/db/LogReader.java:297-383), clean and with byte flips in three blocks.
+  (J/db/LogReader.java:297-383), clean and with byte flips in three blocks;
+  plus a 256 MiB log of 0-40 B records (every block past the walk's 64 event
+  slots: the exact-mode re-walk at scale).
 """
 import numpy as np
 import pytest
@@ -57,11 +59,19 @@ def test_full_size_c3_block_for_block(gpu, jl, oracle):
     assert list(np.nonzero(got2 != got)[0]) == [victim]
 
 
-@pytest.mark.parametrize("payloads", ["c1_1056", "mixed_1b_100k"])
+@pytest.mark.parametrize("payloads", ["c1_1056", "mixed_1b_100k", "short_0_40"])
 def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
     import torch
 
-    lens = wl.c5_lengths(payloads == "mixed_1b_100k", seed=SEED)  # the sets bench.py reports
+    if payloads == "short_0_40":
+        # 0-40 B records, 256 MiB of log: ~1 200 events per 32 KiB block, so
+        # every block overflows the walk's 64 slots (the exact mode re-walks
+        # past them in lc_build), flips included
+        rng = np.random.default_rng(SEED + 11)
+        lens = rng.integers(0, 41, (256 << 20) // 27).astype(np.uint32)
+        lens = lens[: int(np.searchsorted(np.cumsum(lens.astype(np.uint64) + 7), 256 << 20))]
+    else:
+        lens = wl.c5_lengths(payloads == "mixed_1b_100k", seed=SEED)  # the sets bench.py reports
     offs = wl.packed_offsets(lens)
     plan = jl.log_layout(offs, lens)
     src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
@@ -84,7 +94,7 @@ def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
     # flips in three log blocks: a flipped payload byte is BAD_CRC and drops the
     # rest of its 32 KiB block (J/db/LogReader.java:359-367); a flipped header
     # length is a bad-length report.  Either way the walk must match the oracle.
-    for blk in (5, 70_000, (nb >> 15) - 2):
+    for blk in (5, min(70_000, (nb >> 15) - 4), (nb >> 15) - 2):
         log[blk * 32768 + 20_000] ^= 0x01
     w = check()
     assert int(((w["kind"] != 0) & (w["kind"] != jl.LOG_OK)).sum()) >= 3
