@@ -196,11 +196,22 @@ inline std::vector<uint32_t> build_lds_image_v4(int lpb) {
     return img;
 }
 
+// The 8-lane gap step L(x) = G3[x.b0] ^ G2[x.b1] ^ G1[x.b2] ^ G0[x.b3], G_t =
+// z^(124+t)∘T0 (linear): what a chain register still owes after a block's last
+// window.  The gv4 epilogue tables absorb it.
+inline uint32_t gap_step8(uint32_t x) {
+    const Tables &T = tables();
+    uint32_t r = 0;
+    for (int t = 0; t < 4; t++) r ^= T.zn(T.t[0][(x >> (8 * t)) & 0xffu], 124u + 3u - (uint32_t)t);
+    return r;
+}
+
 // General v4 image (general_v4.hip): the v4 image for 8 lanes per block with
 // the epilogue tables re-cut so a block's tail pad d = 16a + 4c + e folds into
 // shifts the epilogue does anyway:
 //   lane tables   column b: z^-(16 (b % 16))   (realign by 16 (l + a))
-//   kG4ShiftDword U_k = z^-(4k), k = 0..6       (chain j: z^-(4 (j + c)))
+//   kG4ShiftDword U_k = z^-(4k) ∘ L, k = 0..6   (chain j: its pending gap step
+//                 L, gap_step8 below, then z^-(4 (j + c)))
 //   kG4EDword     E_e = z^-e, e = 0..3          (after the group xor)
 inline std::vector<uint32_t> build_lds_image_gv4() {
     const Tables &T = tables();
@@ -212,7 +223,7 @@ inline std::vector<uint32_t> build_lds_image_gv4() {
     for (int k = 0; k < 7; k++)
         for (int p = 0; p < 8; p++)
             for (int v = 0; v < 16; v++)
-                img[kG4ShiftDword + (size_t)k * 128 + p * 16 + v] = T.zinvn((uint32_t)v << (4 * p), 4u * (uint32_t)k);
+                img[kG4ShiftDword + (size_t)k * 128 + p * 16 + v] = T.zinvn(gap_step8((uint32_t)v << (4 * p)), 4u * (uint32_t)k);
     for (int e = 0; e < 4; e++)
         for (int p = 0; p < 8; p++)
             for (int v = 0; v < 16; v++)
@@ -246,20 +257,12 @@ inline std::vector<uint32_t> build_lds_image_gv4_rotated() {
 // d mod 16 (bins by (K, d mod 16), log_chunks.hip), so the tail pad's z^-e joins
 // the chain shifts: chain j uses M_m, m = 4 (j + c) + e (28 nibble tables) and
 // the epilogue has no separate z^-e stage.  The tables also absorb the chains'
-// last pending step: after a round's last window a chain register x still owes
-// its lookups, the 8-lane gap step L(x) = G3[x.b0] ^ G2[x.b1] ^ G1[x.b2] ^
-// G0[x.b3] (G_t = z^(124+t)∘T0, linear), so M_m = z^-m ∘ L is applied to the
-// chain registers directly (16 G lookups per round less).  No init / suffix
+// last pending step (gap_step8), so M_m = z^-m ∘ L is applied to the chain
+// registers directly (16 G lookups per round less).  No init / suffix
 // tables (log records are crc'd from value()'s init with no suffix).
 //   byte [16384, 30720)  M_m, m = 0..27, 128 dwords each
 //   byte [30720, 30792)  the front / tail byte selectors (kG4SelDword layout)
 constexpr size_t kLCMDword = 4096, kLCSelDword = 7680;
-inline uint32_t gap_step8(uint32_t x) {  // L above (8 lanes per block: gap 124)
-    const Tables &T = tables();
-    uint32_t r = 0;
-    for (int t = 0; t < 4; t++) r ^= T.zn(T.t[0][(x >> (8 * t)) & 0xffu], 124u + 3u - (uint32_t)t);
-    return r;
-}
 inline std::vector<uint32_t> build_lds_image_logchunk() {
     const Tables &T = tables();
     std::vector<uint32_t> img = build_lds_image_gv4_rotated();

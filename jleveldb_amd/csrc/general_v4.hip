@@ -496,12 +496,11 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                                ushift(lds, x3, sm + 6144u);
             st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
         } else {
-            const uint32_t s0 = gstep_x3(ldsG, x0, gl, 0u), s1 = gstep_x3(ldsG, x1, gl, 0u);
-            const uint32_t s2 = gstep_x3(ldsG, x2, gl, 0u), s3 = gstep_x3(ldsG, x3, gl, 0u);
+            // chain j: its pending gap step, then z^-(4 (j + c)), in one table
             const uint32_t sa = 512u * ((d >> 2) & 3u);
-            const uint32_t c = xor3(ushift(lds, s0, kShiftB + sa), ushift(lds, s1, kShiftB + 512u + sa),
-                                    ushift(lds, s2, kShiftB + 1024u + sa)) ^
-                               ushift(lds, s3, kShiftB + 1536u + sa);
+            const uint32_t c = xor3(ushift(lds, x0, kShiftB + sa), ushift(lds, x1, kShiftB + 512u + sa),
+                                    ushift(lds, x2, kShiftB + 1024u + sa)) ^
+                               ushift(lds, x3, kShiftB + 1536u + sa);
             st = group_xor<8>(realign(lds, c, kLaneB | (col << 2)));
             st = ushift(lds, st, kEB + 512u * (d & 3u));
         }

@@ -143,9 +143,9 @@ static uint32_t emulate_gv4(const std::vector<uint32_t>& img, const uint8_t* blk
                 const int pos = 128 * k + 16 * l + 4 * j;
                 uint32_t w = 0;
                 if (pos >= -4) memcpy(&w, &V[pos + 4], 4);
-                s = gstep_img(img, s ^ w, lane);
+                s = k + 1 < (int)K ? gstep_img(img, s ^ w, lane) : s ^ w;  // the last step stays pending
             }
-            c ^= nib(img, kG4ShiftDword + 128 * (j + ((d >> 2) & 3)), s);
+            c ^= nib(img, kG4ShiftDword + 128 * (j + ((d >> 2) & 3)), s);  // its gap step is in the table
         }
         const uint32_t col = ((l + (d >> 4)) & 15) | ((q & 1) << 4);
         uint32_t r = 0;
