@@ -362,24 +362,28 @@ __global__ __launch_bounds__(256) void lc_combine_kernel(LCArgs A, uint32_t n_bi
     }
 }
 
-// One thread per (block, event mod kLCSlots): only blocks with a failure touch
-// their events.
+// One lane per block checks it; each block with a failure is then rewritten by
+// its whole wave, lane = event (clean logs: one coalesced load per 64 blocks).
 __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t b = t / kLCSlots;
-    const uint32_t j = (uint32_t)(t % kLCSlots);
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
     lc_finish(A);  // the last kernel: the result words the host reads back
-    if (b >= A.n_blocks) return;
-    const uint32_t fb = A.first_bad[b];
-    if (fb == kLCNone) return;
-    const uint32_t cnt = A.count[b];
-    const uint64_t st = A.start[b], bs = b * 32768u;
-    for (uint32_t k = j; k < cnt; k += kLCSlots) {
-        const uint64_t i = st + k;
-        if (i >= A.ev_cap) break;
-        const uint32_t off = (uint32_t)(A.ev[i].offset - bs);
-        if (off == fb) A.ev[i].kind = 2u;       // BAD_CRC ("checksum mismatch")
-        else if (off > fb) A.ev[i].kind = 0u;   // dropped with the rest of the block
+    const uint32_t fb = b < A.n_blocks ? A.first_bad[b] : kLCNone;
+    uint64_t bad = __builtin_amdgcn_ballot_w64(fb != kLCNone);
+    while (bad) {
+        const uint32_t src = (uint32_t)__builtin_ctzll(bad);
+        bad &= bad - 1u;
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)fb, (int)src);
+        const uint64_t bb = b - lane + src;
+        const uint32_t cnt = A.count[bb];
+        const uint64_t st = A.start[bb], bs = bb * 32768u;
+        for (uint32_t k = lane; k < cnt; k += 64u) {
+            const uint64_t i = st + k;
+            if (i >= A.ev_cap) break;
+            const uint32_t off = (uint32_t)(A.ev[i].offset - bs);
+            if (off == f) A.ev[i].kind = 2u;      // BAD_CRC ("checksum mismatch")
+            else if (off > f) A.ev[i].kind = 0u;  // dropped with the rest of the block
+        }
     }
 }
 
@@ -397,11 +401,11 @@ hipError_t launch_lc_build(const LCArgs &A, hipStream_t st) {
 }
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st) {
     const uint32_t nmax = (uint32_t)(A.big_cap < 0xffffffffull ? A.big_cap : 0xffffffffull);
-    hipLaunchKernelGGL(lc_combine_kernel, dim3(1024), dim3(256), 0, st, A, nmax);
+    hipLaunchKernelGGL(lc_combine_kernel, dim3(256), dim3(256), 0, st, A, nmax);
     return hipGetLastError();
 }
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st) {
-    const uint64_t n = (uint64_t)A.n_blocks * kLCSlots;
+    const uint64_t n = (uint64_t)A.n_blocks;
     hipLaunchKernelGGL(lc_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A);
     return hipGetLastError();
 }
