@@ -287,8 +287,6 @@ def copy_inclusive_c2(data):
     t0 = time.perf_counter()
     jl.crc32c_fixed(pinned, 4096)
     pin_s = time.perf_counter() - t0
-    pageable = pinned.numpy().copy()
-    del pinned
     # the link's own ceiling on this box: one plain pinned H2D copy of the same bytes
     dev_buf = torch.empty(nbytes, dtype=torch.uint8, device=data.device)
     dev_buf[: 64 << 20].copy_(pinned[: 64 << 20])  # warm the DMA path
@@ -298,6 +296,8 @@ def copy_inclusive_c2(data):
     torch.cuda.synchronize()
     h2d_s = time.perf_counter() - t0
     del dev_buf
+    pageable = pinned.numpy().copy()
+    del pinned
     res = {"config": "C2 from host memory (H2D + kernel + D2H, 64 MiB chunks, double-buffered)",
            "pinned_GiB_per_s": round(nbytes / pin_s / GIB, 2),
            "h2d_copy_ceiling_GiB_per_s": round(nbytes / h2d_s / GIB, 2)}
