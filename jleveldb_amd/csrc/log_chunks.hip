@@ -243,6 +243,69 @@ __device__ __forceinline__ void lc_place(const LCArgs &A, uint32_t *ctr, const u
     }
 }
 
+__device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v);
+
+// lc_place for a whole wave, one record per lane (ok false: none), all lanes
+// calling: a one-chunk record places its descriptor from its own lane; the
+// chunks of longer records are spread over the wave's lanes (lane c takes
+// chunk c of the wave's chunk list, its record found by a binary search over
+// the lanes' chunk offsets) instead of one lane placing its record's J chunks
+// in turn.
+__device__ __forceinline__ void lc_place_wave(const LCArgs &A, uint32_t *ctr, const uint32_t *rs, bool ok,
+                                              uint64_t prel, uint32_t n, uint32_t stored) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    LCGeom g{0u, 0u, 0u, 0u};
+    if (ok) g = lc_geom((uint64_t)(uintptr_t)A.log + prel, n);
+    if (ok && g.J == 1u) lc_desc(A, rs, g.K, atomicAdd(&ctr[lc_bin(g.K, g.r)], 1u), prel, 1u, g.r, 0u, stored);
+    const bool multi = ok && g.J > 1u;
+    if (__builtin_amdgcn_ballot_w64(multi) == 0ull) return;
+    uint32_t pi = 0, fits = 0;
+    if (multi) {
+        const uint32_t bi = atomicAdd(&ctr[kLCBig], 1u);
+        pi = atomicAdd(&ctr[kLCPart], g.J);
+        // past a capacity (cannot happen with the caller's bounds) the chunks still
+        // take their ranks, as empty groups: no round of the table is left unwritten
+        fits = bi < A.big_cap && (uint64_t)pi + g.J <= A.part_cap;
+        if (fits) {
+            LCBig big;
+            big.p = prel;
+            big.n = n;
+            big.stored = stored;
+            big.part0 = pi;
+            big.J = g.J;
+            A.big[bi] = big;
+        } else {
+            atomicOr(A.cap_flag, 1u);
+            if (bi < A.big_cap) A.big[bi].J = 0u;  // skipped by lc_combine
+        }
+    }
+    const uint32_t m = multi ? g.J : 0u;
+    const uint32_t off = lc_wave_excl_sum(m);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(off + m), 63);
+    for (uint32_t c0 = 0; c0 < total; c0 += 64u) {
+        const uint32_t c = c0 + lane;
+        uint32_t o = 0;  // the last lane whose chunk offset is <= c: chunk c's record
+        for (uint32_t s = 32u; s; s >>= 1) {
+            const uint32_t cand = o + s;
+            if ((uint32_t)__shfl((int)off, (int)cand) <= c) o = cand;
+        }
+        const uint32_t j = c - (uint32_t)__shfl((int)off, (int)o);
+        const uint32_t J = (uint32_t)__shfl((int)g.J, (int)o), Kr = (uint32_t)__shfl((int)g.K, (int)o);
+        const uint32_t r = (uint32_t)__shfl((int)g.r, (int)o), f = (uint32_t)__shfl((int)g.f, (int)o);
+        const uint32_t p0 = (uint32_t)__shfl((int)pi, (int)o), ft = (uint32_t)__shfl((int)fits, (int)o);
+        const uint64_t pr = (uint64_t)(uint32_t)__shfl((int)(uint32_t)prel, (int)o) |
+                            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(prel >> 32), (int)o) << 32);
+        if (c < total) {
+            const bool last = j + 1u == J;
+            const uint32_t K = last ? Kr - kLCWin * j : kLCWin;
+            const uint32_t d = last ? r : 0u;
+            const uint32_t rank = atomicAdd(&ctr[lc_bin(K, d)], 1u);
+            // chunks j >= 1 start on the grid, at the record's first window + 4096 j
+            lc_desc(A, rs, K, rank, j ? pr - f + 4096ull * j : pr, j == 0u, d, ft ? kGPart | (p0 + j) : kGNull, 0u);
+        }
+    }
+}
+
 __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t off, uint32_t length, uint32_t type,
                                          uint32_t kind) {
     if (at >= A.ev_cap) return;
@@ -311,7 +374,7 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         const uint32_t stored = (uint32_t)(s >> 32);
         const uint64_t h = bs + lc_wave_excl_sum(have ? 7u + length : 0u);  // this event's header
         if (have) lc_event(A, st[i] + lane, h, length, type, kind);
-        if (A.checksum) lc_place(A, ctr, rs, have && kind == 1u, h + 6u, 1u + length, stored);
+        if (A.checksum) lc_place_wave(A, ctr, rs, have && kind == 1u, h + 6u, 1u + length, stored);
         if (cnt[i] <= kLCSlots || !A.exact) continue;
         // exact mode: the events past the slots (a block of many short records)
         // are walked again by lane 0 from the header after the last kept one (an
