@@ -109,9 +109,14 @@ struct Workspace {
     hipStream_t stream = nullptr;  // compute stream of the host-memory entry points
     DevBuf ws_lc, ws_slot, ws_desc, ws_big, ws_part, ws_tmp;  // chunked log verify (log_chunks.hip)
     DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
+    // the chunked log verify's result words: coherent host memory the last kernel
+    // writes directly (no D2H copy of them, the host polls the stream)
+    uint64_t *h_res = nullptr;
     Slot slot[2];
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (h_res) (void)hipHostFree(h_res);
+        h_res = nullptr;
         for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_ls, &ws_lsev})
             b->release();
         for (Slot &sl : slot) {
@@ -1131,6 +1136,15 @@ static int log_verify_stream(Workspace &c, const void *d_log, uint64_t log_bytes
 // block (records of ~512 B and up); a log with a block of more events sets
 // *redo and the caller runs the exact mode, which reads the chunk totals back
 // after the walk and re-walks the blocks past their slots.
+// Waits for the stream's work by polling it (hipStreamQuery) instead of a
+// blocking synchronise.
+static hipError_t poll_stream(hipStream_t st) {
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+    }
+}
+
 static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum, int exact,
                              jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo) {
     *redo = false;
@@ -1160,7 +1174,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.rstart = (uint32_t *)(ws + o_rs);
     A.first_bad = (uint32_t *)(ws + o_fb);
     A.cap_flag = (uint32_t *)(ws + o_flag);
-    A.result = (uint64_t *)(ws + o_res);
+    if (!c.h_res) JL_HIP(hipHostMalloc((void **)&c.h_res, 64, hipHostMallocCoherent));
+    A.result = c.h_res;
     A.ev = (jlk::LogEvent *)d_events;
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
@@ -1214,9 +1229,12 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));
     }
-    uint64_t res[3] = {0, 0, 0};  // events, blocks past their slots, capacity flag (lc_finish)
-    JL_HIP(hipMemcpyAsync(res, A.result, sizeof(res), hipMemcpyDeviceToHost, st));
-    JL_HIP(hipStreamSynchronize(st));
+    // events, blocks past their slots, capacity flag (lc_finish, written to c.h_res
+    // by the last kernel): wait by polling the stream (a blocking synchronise
+    // sleeps, and a D2H copy of the words cost ~50 us between back-to-back calls)
+    JL_HIP(poll_stream(st));
+    const volatile uint64_t *hr = c.h_res;
+    const uint64_t res[3] = {hr[0], hr[1], hr[2]};
     if (res[1] && !exact) {
         *redo = true;
         return JL_OK;
