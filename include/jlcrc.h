@@ -232,6 +232,19 @@ typedef struct jl_log_event {
 #define JL_LOG_CHECKSUM_FUSED 3
 int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                       uint64_t *n_events, void *stream);
+/* Asynchronous form of jl_log_verify_dev (same path and events): returns once
+ * the kernels are enqueued on `stream`; the result words land in device memory
+ * d_result[3] in stream order: [0] the event total (events past `cap` are not
+ * written), [1] blocks holding more than the walk's 64 event slots — when
+ * non-zero the events are incomplete and the log must be verified again with
+ * jl_log_verify_dev, which re-walks such blocks —, [2] non-zero if an internal
+ * capacity was exceeded (likewise).  checksum: JL_LOG_NO_CHECKSUM,
+ * JL_LOG_CHECKSUM or JL_LOG_CHECKSUM_TWO_PASS.  A thread's log calls share its
+ * scratch: a call on another stream first waits for this one.  Lets a caller
+ * keep several verifications in flight back to back (no host round trip per
+ * log); replaces the same readPhysicalRecord loop (J/db/LogReader.java:297-383). */
+int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
+                            uint64_t *d_result, void *stream);
 /* Host-memory form (log = the on-disk .log / MANIFEST bytes); blocking. */
 int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_event *events, uint64_t cap,
                   uint64_t *n_events);

@@ -90,6 +90,7 @@ def lib() -> ctypes.CDLL:
         "jl_table_verify": (i32, [vp, u64, vp, vp, u64, vp]),
         "jl_table_block_handles": (i32, [vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_verify_dev": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64), vp]),
+        "jl_log_verify_dev_async": (i32, [vp, u64, i32, vp, u64, vp, vp]),
         "jl_log_verify": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_read_records": (i32, [vp, u64, i32, u64, vp, u64, vp, u64, ctypes.POINTER(u64), vp, u64,
                                       ctypes.POINTER(u64)]),
@@ -443,6 +444,21 @@ def log_verify_dev(log, checksum: bool = True, events=None, stream=None):
                                      _stream(stream))
     _check(rc, "jl_log_verify_dev")
     return events, n.value
+
+
+def log_verify_dev_async(log, checksum: bool = True, events=None, result=None, stream=None):
+    """Asynchronous device-resident verification (jl_log_verify_dev_async): enqueues
+    the kernels and returns (events, result) at once; result (3 x int64 on the
+    device, filled in stream order) = [events, blocks past the walk's slots,
+    capacity flag] — when [1] or [2] is non-zero use log_verify_dev instead."""
+    import torch
+
+    if result is None:
+        result = torch.empty(3, dtype=torch.int64, device=log.device)
+    cap = 0 if events is None else events.numel() // LOG_EVENT_DTYPE.itemsize
+    _check(lib().jl_log_verify_dev_async(_dptr(log), log.numel(), int(checksum), _dptr(events), cap, _dptr(result),
+                                         _stream(stream)), "jl_log_verify_dev_async")
+    return events, result
 
 
 def log_read_records(log, checksum: bool = True, initial_offset: int = 0):

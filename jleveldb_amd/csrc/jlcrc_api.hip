@@ -112,6 +112,7 @@ struct Workspace {
     // the chunked log verify's result words: coherent host memory the last kernel
     // writes directly (no D2H copy of them, the host polls the stream)
     uint64_t *h_res = nullptr;
+    hipStream_t async_st = nullptr;  // stream of the last jl_log_verify_dev_async still possibly in flight
     Slot slot[2];
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -1145,8 +1146,12 @@ static hipError_t poll_stream(hipStream_t st) {
     }
 }
 
+// d_result null: synchronous (the count read back, *redo set when a block
+// overflowed its slots); else asynchronous: the result words go to d_result
+// on the stream and the call returns after the launches.
 static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum, int exact,
-                             jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo) {
+                             jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo,
+                             uint64_t *d_result = nullptr) {
     *redo = false;
     if (log_bytes >= (1ull << 40)) return fail(JL_ERR_INVALID, "jl_log_verify: log larger than 1 TiB");
     const uint64_t nb = (log_bytes + 32767) / 32768, ng = (nb + jlk::kLCGroup - 1) / jlk::kLCGroup;
@@ -1175,7 +1180,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.first_bad = (uint32_t *)(ws + o_fb);
     A.cap_flag = (uint32_t *)(ws + o_flag);
     if (!c.h_res) JL_HIP(hipHostMalloc((void **)&c.h_res, 64, hipHostMallocCoherent));
-    A.result = c.h_res;
+    A.result = d_result ? d_result : c.h_res;
     A.ev = (jlk::LogEvent *)d_events;
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
@@ -1229,6 +1234,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));
     }
+    if (d_result) return JL_OK;  // asynchronous: the caller reads d_result in stream order
     // events, blocks past their slots, capacity flag (lc_finish, written to c.h_res
     // by the last kernel): wait by polling the stream (a blocking synchronise
     // sleeps, and a D2H copy of the words cost ~50 us between back-to-back calls)
@@ -1273,6 +1279,14 @@ static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, 
     return JL_OK;
 }
 
+// The log-verify scratch of a workspace is reused by every call of its thread:
+// asynchronous calls left in flight on another stream are finished first.
+static int ws_order(Workspace &w, hipStream_t st, bool async) {
+    if (w.async_st && w.async_st != st) JL_HIP(hipStreamSynchronize(w.async_st));
+    w.async_st = async ? st : nullptr;
+    return JL_OK;
+}
+
 int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                       uint64_t *n_events, void *stream) {
     if (int r = ensure_ready()) return r;
@@ -1280,7 +1294,29 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
     if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify_dev: bad checksum mode");
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
-    return log_verify_impl(*w, d_log, log_bytes, checksum, d_events, cap, n_events, pick(stream), true);
+    const hipStream_t st = pick(stream);
+    if (int r = ws_order(*w, st, false)) return r;
+    return log_verify_impl(*w, d_log, log_bytes, checksum, d_events, cap, n_events, st, true);
+}
+
+int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
+                            uint64_t *d_result, void *stream) {
+    if (int r = ensure_ready()) return r;
+    if (!d_result || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev_async: null pointer");
+    if (checksum < 0 || checksum > JL_LOG_CHECKSUM_TWO_PASS)
+        return fail(JL_ERR_INVALID, "jl_log_verify_dev_async: bad checksum mode");
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    const hipStream_t st = pick(stream);
+    if (int r = ws_order(*w, st, true)) return r;
+    if (log_bytes == 0) {
+        JL_HIP(hipMemsetAsync(d_result, 0, 3 * sizeof(uint64_t), st));
+        return JL_OK;
+    }
+    bool redo = false;
+    uint64_t n = 0;
+    return log_verify_chunks(*w, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, 0, d_events, cap, &n, st, &redo,
+                             d_result);
 }
 
 // Host-memory log verification: chunks of JL_STREAM_CHUNK_BYTES (whole 32 KiB
@@ -1297,6 +1333,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     if (log_bytes == 0) return JL_OK;
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
+    if (int r = ws_order(*w, w->stream, false)) return r;
     const uint64_t CH = JL_STREAM_CHUNK_BYTES, first = std::min(CH, log_bytes);
     const uint64_t ev_cap = first / 7 + 2;  // upper bound on a chunk's physical records
     for (Slot &sl : w->slot) {

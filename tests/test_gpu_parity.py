@@ -310,6 +310,39 @@ def test_log_dev_resident(gpu, jl, oracle):
     assert _events(got) == _events(oracle.log_events(log))
 
 
+def test_log_dev_async(gpu, jl, oracle):
+    """jl_log_verify_dev_async: several logs verified back to back on one stream
+    with no host round trip (a corrupted one, a tiny one, an empty one), then
+    checked against the oracle from their device result words; a log with more
+    than 64 records in a block reports it in result[1] (verify it with the
+    synchronous call)."""
+    import torch
+
+    rng = np.random.default_rng(41)
+    logs = []
+    for n, mx, flips in ((2000, 3000, 5), (300, 70000, 3), (3, 50, 0)):
+        _, log = _random_log(oracle, rng, n, mx)
+        log = bytearray(log)
+        for _ in range(flips):
+            log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
+        logs.append(bytes(log))
+    logs.append(b"")
+    runs = []
+    for log in logs:
+        d = to_dev(np.frombuffer(log, np.uint8), gpu) if log else torch.empty(0, dtype=torch.uint8, device=gpu)
+        ev = torch.empty((len(log) // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
+        runs.append((log, d, *jl.log_verify_dev_async(d, True, events=ev)))
+    for log, d, ev, res in runs:
+        n, over, capf = (int(x) for x in res.cpu().numpy())
+        assert over == 0 and capf == 0
+        got = np.frombuffer(ev.cpu().numpy().tobytes()[: n * 16], dtype=jl.LOG_EVENT_DTYPE)
+        assert _events(got) == _events(oracle.log_events(log))
+    payloads = [bytes(int(s)) for s in rng.integers(0, 30, 3000)]
+    d = to_dev(np.frombuffer(oracle.log_write(payloads), np.uint8), gpu)
+    _, res = jl.log_verify_dev_async(d, True, events=torch.empty(16 * 8000, dtype=torch.uint8, device=gpu))
+    assert int(res[1]) > 0  # blocks past the walk's slots: the caller re-verifies synchronously
+
+
 # ----------------------------------------------------------------- helpers
 def test_fill_random_matches_oracle(gpu, jl, oracle):
     import torch

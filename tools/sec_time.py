@@ -24,5 +24,5 @@ if which in ("all", "c3"):
 if which in ("all", "c5"):
     for mixed in (False, True):
         r = bench.secondary_c5(dev, stream, steps, 3, mixed=mixed, cpu=False, host_copy=False)
-        print(json.dumps({k: r[k] for k in ("config", "GiB_per_s", "ms_per_step", "records_ok") if k in r}), flush=True)
+        print(json.dumps({k: r[k] for k in ("config", "GiB_per_s", "ms_per_step", "records_ok", "sync_call", "async_events_equal_sync") if k in r}), flush=True)
         torch.cuda.empty_cache()
