@@ -323,13 +323,18 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
 // event j (coalesced slot reads and event writes; the header offsets are the
 // prefix sums of 7 + length over the lanes).
 constexpr uint32_t kLCBuildWaves = 4;  // 16 blocks per wave, all their loads issued first: one occupancy batch
+// Exclusive prefix sum over the wave's 64 lanes with DPP only (no LDS
+// crossbar round trips): Hillis-Steele inside each row of 16 (row_shr 1/2/4/8),
+// then the row totals through row_bcast:15 (rows 1, 3) and row_bcast:31 (rows
+// 2, 3).  Lanes without a source add the `old` operand, 0.  All lanes active.
 __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     uint32_t x = v;
-    for (uint32_t o = 1; o < 64u; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-        if (lane >= o) x += y;
-    }
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x - v;
 }
 
