@@ -147,6 +147,8 @@ struct RoundView {
     uint32_t idx;  // per lane (kGNull: no result)
     uint32_t K;    // wave-uniform
     uint32_t stored, seed;  // MODE_LOG_CHUNK: per lane, the group's stored crc and seed flag
+    uint32_t f;             // MODE_LOG_CHUNK: p & 127 (p itself is dead in the round loop; a
+                            // failure re-reads it from the descriptor)
 };
 
 __device__ __forceinline__ uint32_t sel8(uint32_t q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t a4,
@@ -160,6 +162,7 @@ template <int MODE>
 __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, uint32_t q) {
     RoundView v;
     v.stored = 0;
+    v.f = 0;
     v.seed = 0;
     if (A.desc) {
         // the round's 8 descriptors (128 B) with two scalar loads: SMEM/lgkmcnt, so the
@@ -195,6 +198,7 @@ __device__ __forceinline__ RoundView round_view(const GV4Args &A, uint32_t r, ui
             v.K = (w[1] >> 8) & 0xffu;
             v.p = (uint64_t)(uintptr_t)A.P.base + (((uint64_t)(hi & 0xffu) << 32) | lo);
             v.seed = (hi >> 16) & 1u;
+            v.f = (uint32_t)(v.p & 127u);
             v.stored = sel8(q, w[3], w[7], w[11], w[15], w[19], w[23], w[27], w[31]);
         }
     } else {  // 128-B aligned base and stride (run_gv4): f = d = 0
@@ -243,11 +247,13 @@ __device__ __forceinline__ RoundView desc_read(const GV4Args &A, uint32_t set) {
     v.idx = ix;
     v.K = (uint32_t)__builtin_amdgcn_readlane((int)k, 0);
     v.stored = 0;
+    v.f = 0;
     v.seed = 0;
     if constexpr (GV4<MODE>::LOGC) {
         v.K = (uint32_t)__builtin_amdgcn_readlane((int)((hi >> 8) & 0xffu), 0);
         v.p = (uint64_t)(uintptr_t)A.P.base + (((uint64_t)(hi & 0xffu) << 32) | lo);
         v.seed = (hi >> 16) & 1u;
+        v.f = (uint32_t)(v.p & 127u);
         v.stored = k;
     }
     return v;
@@ -457,7 +463,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             side_c = wv;
             return;
         }
-        const uint32_t f = (uint32_t)(cv.p & 127u);
+        const uint32_t f = GV4<MODE>::LOGC ? cv.f : (uint32_t)(cv.p & 127u);
         uint32_t v[4] = {wv.x, wv.y, wv.z, wv.w};
         // byte selectors from the image (kG4SelByte): v_med3 + one LDS read + v_perm per
         // dword, no divergent shift code
@@ -556,7 +562,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                 if (cv.idx >= kGPart) {
                     A.parts[cv.idx - kGPart] = raw;
                 } else if (m != cv.stored) {  // rare: first_bad[block] = min(header offset in the block)
-                    const uint64_t h = p - 6u - (uint64_t)(uintptr_t)A.P.base;
+                    // the chunk's offset from its descriptor (a rare vector load: the
+                    // compiler's vmcnt(0) before its use only drains the ring here)
+                    const uint64_t h = (A.desc[(uint64_t)cr * 8u + q].pd & 0xffffffffffull) - 6u;
                     atomicMin(A.P.out32 + (h >> 15), (uint32_t)(h & 32767u));
                 }
             } else if (MODE == MODE_CRC) {
