@@ -322,7 +322,12 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
 // ranges per bin come from the scan): one wave per block at a time, lane j =
 // event j (coalesced slot reads and event writes; the header offsets are the
 // prefix sums of 7 + length over the lanes).
-constexpr uint32_t kLCBuildWaves = 4;  // 16 blocks per wave, all their loads issued first: one occupancy batch
+#ifndef JL_LC_BUILD_WAVES
+#define JL_LC_BUILD_WAVES 8
+#endif
+// 8 blocks per wave, all their loads issued first (r2: 8 waves x 8 blocks ran
+// lc_build 77 -> 63 us against 4 x 16, C5 ~3 % faster; 16 x 4 about the same)
+constexpr uint32_t kLCBuildWaves = JL_LC_BUILD_WAVES;
 // Exclusive prefix sum over the wave's 64 lanes with DPP only (no LDS
 // crossbar round trips): Hillis-Steele inside each row of 16 (row_shr 1/2/4/8),
 // then the row totals through row_bcast:15 (rows 1, 3) and row_bcast:31 (rows
