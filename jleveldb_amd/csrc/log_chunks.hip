@@ -99,7 +99,7 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
 constexpr uint32_t kLCLdsSlots = 34;
 __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     __shared__ uint32_t h[4][kLCCounters];
-    __shared__ uint64_t ls[kLCLdsSlots][256];  // [slot][thread]: conflict-free writes
+    __shared__ uint64_t ls[256][kLCLdsSlots + 1];  // [thread][slot], padded: the write-back reads it in order
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) (&h[0][0])[i] = 0;
     __syncthreads();
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
             const uint32_t stored = (uint32_t)hv;
             if (!d.stop && be - pn >= 7) hv = lc_header(A.log + pn, be - pn);
             const uint64_t slot = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
-            if (cnt < kLCLdsSlots) ls[cnt][threadIdx.x] = slot;
+            if (cnt < kLCLdsSlots) ls[threadIdx.x][cnt] = slot;
             else if (cnt < kLCSlots) A.slots[b * kLCSlots + cnt] = slot;
             // chunk histogram: exactly the chunks lc_build places (in the fast
             // mode only the kept events: a block that overflows its slots makes
@@ -148,9 +148,15 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         if (cnt > kLCSlots) atomicAdd(&h[wv][kLCOver], 1u);
     }
     __syncthreads();
-    // the LDS slots out: slot j of the workgroup's 256 blocks
-    const uint32_t kept = cnt < kLCLdsSlots ? cnt : kLCLdsSlots;
-    for (uint32_t j = 0; j < kept; j++) A.slots[b * kLCSlots + j] = ls[j][threadIdx.x];
+    // the LDS slots out, the workgroup's 256 blocks together: consecutive threads
+    // store a block's consecutive slots (a run of kLCLdsSlots x 8 B per block; one
+    // thread per block writing its own slots touched 64 lines per store, 33 us of
+    // the C5 walk).  Slots past a block's count are never read.
+    const uint64_t b0 = (uint64_t)blockIdx.x * 256u;
+    for (uint32_t e = threadIdx.x; e < 256u * kLCLdsSlots; e += 256u) {
+        const uint32_t t = e / kLCLdsSlots, j = e - t * kLCLdsSlots;
+        if (b0 + t < A.n_blocks) A.slots[(b0 + t) * kLCSlots + j] = ls[t][j];
+    }
     const uint64_t g0 = (uint64_t)blockIdx.x * 4u;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) {
         const uint32_t g = i % 4u, c = i / 4u;  // 4 consecutive groups of one counter: one 16-B run
