@@ -86,8 +86,34 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs the cgroup's CFS quota allows (cpu.max / cpu.cfs_quota_us), or None."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), open(
+                            "/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()])):
+        try:
+            with open(path) as f:
+                q, per = parse(f.read())[:2]
+            if q not in ("max", "-1") and int(per) > 0:
+                return max(1, int(q) // int(per))
+        except (OSError, ValueError, IndexError):
+            continue
+    return None
+
+
 def cpu_threads() -> int:
-    return min(16, os.cpu_count() or 1)
+    """Threads of the all-cores CPU legs: the CPUs this process may run on
+    (sched_getaffinity), bounded by the cgroup's CPU quota when it sets one (more
+    threads than the quota only time-slice the same cores)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    q = cpu_quota()
+    return max(1, min(n, q) if q else n)
+
+
+def cpu_context() -> dict:
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": cpu_model(), "affinity_cpus": aff, "cgroup_cpu_quota": cpu_quota(),
+            "os_cpu_count": os.cpu_count()}
 
 
 def best_host_rate(host: np.ndarray, seconds: float = 3.0) -> dict:
@@ -139,7 +165,7 @@ def cpu_baseline(data, n_blocks, gpu_out, seconds):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "cpu_model": cpu_model(),
+        **cpu_context(),
         "sample": f"{sample_blocks} x 4 KiB blocks (1 GiB) of the same data, {done} passes in {el:.1f} s; "
                   f"oracle/crc32c_oracle.c slicing-by-8 restatement of Crc32C.update; 1-thread rate {one:.2f} GiB/s",
         "one_thread_GiB_per_s": round(one, 3),
@@ -179,31 +205,37 @@ def secondary_c3(dev, stream, steps, warmup, cpu=True):
             oracle.batch(sub, offs[:k], lens[:k], threads=th)
             legs[th] = sub.size / (time.perf_counter() - t0) / GIB
         res["cpu_baseline"] = {"GiB_per_s": round(legs[cpu_threads()], 3), "cores": cpu_threads(),
-                               "one_thread_GiB_per_s": round(legs[1], 3), "kind": "port", "cpu_model": cpu_model(),
+                               "one_thread_GiB_per_s": round(legs[1], 3), "kind": "port", **cpu_context(),
                                "sample": f"the first {k} blocks ({sub.size / GIB:.2f} GiB) of the same arena, "
                                          "oracle slicing-by-8 batch", "parity_with_gpu": parity}
     del arena
     return res
 
 
-def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True, host_copy=True):
+C5_LABELS = {
+    "c1_1056": "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident",
+    "mixed_1b_100k": "C5 WAL verify, 2^17 x 32 KiB blocks, mixed 1 B-100 KiB records (fragmented), device-resident",
+    "dbbench_131": "C5 WAL verify, 2^17 x 32 KiB blocks, DBBench-default 131-B records (16-B key + 100-B value, "
+                   "DBBench.java:80; ~237 per block, every block dense), device-resident",
+}
+
+
+def secondary_c5(dev, stream, steps, warmup, which="c1_1056", cpu=True, host_copy=True):
     """Config C5: streaming WAL verification over 2^17 x 32 KiB log blocks (4 GiB).
 
     The log is produced on the device by the product's batched LogWriter
     (jl_log_layout + jl_log_emit_dev), then verified with jl_log_verify_dev
     (header walk + per-record masked-CRC check with
-    LogReader.readPhysicalRecord semantics).  Two payload sets (SURVEY.md
-    §8d C5): C1-shaped records (1 056-B payload = 12-B batch header + 16-B key
-    + 1 KiB value), and a mixed 1 B-100 KiB set whose records fragment into
-    FIRST/MIDDLE/LAST across log blocks.  Timed device-resident, and
-    copy-inclusive from pinned host memory through jl_log_verify; the CPU
-    leg times the oracle's readPhysicalRecord walk (1 thread) on the first
-    1 GiB of the same log."""
-    lens = wl.c5_lengths(mixed, seed=SEED)
-    if mixed:
-        label = "C5 WAL verify, 2^17 x 32 KiB blocks, mixed 1 B-100 KiB records (fragmented), device-resident"
-    else:
-        label = "C5 WAL verify, 2^17 x 32 KiB blocks, 1 056-B records, device-resident"
+    LogReader.readPhysicalRecord semantics).  Three payload sets: C1-shaped
+    records (1 056-B payload = 12-B batch header + 16-B key + 1 KiB value) and a
+    mixed 1 B-100 KiB set whose records fragment into FIRST/MIDDLE/LAST across
+    log blocks, and DBBench's default write (16-B key,
+    100-B value: 131-B payloads, every 32 KiB block dense).  Timed
+    device-resident, and copy-inclusive from pinned and pageable host memory
+    through jl_log_verify; the CPU legs time the oracle's readPhysicalRecord
+    walk on the first 1 GiB of the same log (1 thread and all threads)."""
+    lens = wl.c5_lengths(which, seed=SEED)
+    label = C5_LABELS[which]
     offs = wl.packed_offsets(lens)
     plan = jl.log_layout(offs, lens)
     src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=dev)
@@ -225,14 +257,15 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True, host_copy=Tr
         fa()
     wall, ms = timed(fa, steps, warmup, stream)
     r = result.cpu().numpy()
-    same_async = int(r[0]) == n_ev and int(r[1]) == 0 and int(r[2]) == 0 and torch.equal(
+    same_async = int(r[0]) == n_ev and int(r[2]) == 0 and torch.equal(
         events[: n_ev * 16].view(-1, 16)[:, 13].cpu(), torch.from_numpy(kinds))
     _, ms_sync = timed(fn, steps, warmup, stream)
     alg = crc_bytes + 7 * plan["len"].size
     res = {"config": label, "log_bytes": nb, "payload_records": int(lens.size),
-           "physical_records": int(plan["len"].size), "records_ok": ok,
-           "path": "header walk + record chunks in exact (K, d) rounds through general v4 + fold/apply (JL_LOG_CHECKSUM), "
-                   "jl_log_verify_dev_async back to back",
+           "physical_records": int(plan["len"].size), "records_ok": ok, "dense_blocks": int(r[1]),
+           "path": "header walk + record chunks in exact (K, d) rounds through general v4 + fold/apply, dense blocks "
+                   "(> 64 records) whole from LDS (JL_LOG_CHECKSUM), jl_log_verify_dev_async back to back",
+           "achieved_frac_of_peak": round(alg / (ms / steps / 1e3) / 1e9 / PEAK_GBS, 4),
            "GiB_per_s": round(nb / (ms / steps / 1e3) / GIB, 1),
            "achieved_GBps": round(alg / (ms / steps / 1e3) / 1e9, 1),
            "ms_per_step": round(ms / steps, 3), "wall_ms_per_step": round(wall / steps * 1e3, 3),
@@ -285,11 +318,61 @@ def secondary_c5(dev, stream, steps, warmup, mixed=False, cpu=True, host_copy=Tr
             allc = sample.size / (time.perf_counter() - t0) / GIB
         ok_all = sum(int((p["kind"] == jl.LOG_OK).sum()) for p in parts)
         res["cpu_baseline"] = {"GiB_per_s": round(allc, 3), "cores": th, "one_thread_GiB_per_s": round(one, 3),
-                               "kind": "port", "cpu_model": cpu_model(),
+                               "kind": "port", **cpu_context(),
                                "sample": "first 1 GiB of the same log, oracle readPhysicalRecord walk + CRC "
                                          f"({th} threads over 32 KiB-block-aligned pieces, and 1 thread)",
                                "records_ok": int((want["kind"] == jl.LOG_OK).sum()),
                                "records_ok_threaded": ok_all}
+    return res
+
+
+def dispatch_latency(oracle_free=True):
+    """Per-call latency at the reference's call granularity (host memory, as an
+    mmap'd file): one table of ~4.2 KB blocks (Options.java:206,208: 4 KiB blocks,
+    2 MiB tables) and one WAL of 1 056-B records (Options.java:203: 4 MiB write
+    buffer), at several sizes, through the device path (JL_OPT_HOST_THRESHOLD 0)
+    and the host SSE4.2 path (threshold above the size).  Median of repeated calls;
+    the crossover is the smallest size from which the device is faster."""
+    rng = np.random.default_rng(SEED + 17)
+    prev = (jl.get_option(jl.OPT_HOST_THRESHOLD), jl.get_option(jl.OPT_LOG_HOST_THRESHOLD))
+
+    def med(fn, reps):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)) * 1e6
+
+    res = {"table": [], "log": []}
+    for mib in (0.25, 1, 2, 4, 8, 16, 64):
+        nbytes = int(mib * (1 << 20))
+        sizes = rng.integers(3900, 4400, max(1, nbytes // 4150)).astype(np.uint32)
+        offs = wl.packed_offsets(sizes + 5)
+        table = rng.integers(0, 256, int(offs[-1]) + int(sizes[-1]) + 5, dtype=np.uint8)
+        lens = np.full(max(1, nbytes // (wl.C1_PAYLOAD + 7)), wl.C1_PAYLOAD, np.uint32)
+        plan = jl.log_layout(wl.packed_offsets(lens), lens)
+        src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device="cuda")
+        jl.fill_random_dev(src, SEED + 19)
+        log = jl.log_emit_dev(src, plan).cpu().numpy().copy()
+        reps = 30 if mib <= 4 else 8
+        row_t, row_l = {"MiB": mib}, {"MiB": mib}
+        for path, thr in (("device_us", 0), ("host_us", 1 << 40)):
+            jl.set_option(jl.OPT_HOST_THRESHOLD, thr)
+            jl.set_option(jl.OPT_LOG_HOST_THRESHOLD, thr)
+            row_t[path] = round(med(lambda: jl.table_verify(table, offs, sizes), reps), 1)
+            row_l[path] = round(med(lambda: jl.log_verify(log), reps), 1)
+        res["table"].append(row_t)
+        res["log"].append(row_l)
+    jl.set_option(jl.OPT_HOST_THRESHOLD, prev[0])
+    jl.set_option(jl.OPT_LOG_HOST_THRESHOLD, prev[1])
+    for k in ("table", "log"):
+        faster = [r["MiB"] for r in res[k] if r["device_us"] < r["host_us"]]
+        res[f"{k}_crossover_MiB"] = min(faster) if faster else None
+    res["config"] = ("per-call latency, host-memory input (pageable), device path vs the host SSE4.2 path: one table "
+                     "of ~4.2 KB blocks and one WAL of 1 056-B records per call, 1 calling thread")
+    res["host_threshold_default_bytes"] = {"tables_batches": prev[0], "logs": prev[1]}
     return res
 
 
@@ -331,16 +414,39 @@ def copy_inclusive_c2(data):
     return res
 
 
-def spawn_ranks(gpus: int) -> None:
+def visible_gpus() -> int:
+    """GPUs this process would see, counted WITHOUT initialising HIP (the parent
+    of the ranks must not touch the GPU): the *_VISIBLE_DEVICES lists when set,
+    else the GPU nodes of the KFD topology (nodes with SIMDs)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    n = 0
+    for props in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(props) as f:
+                for line in f:
+                    k, _, val = line.partition(" ")
+                    if k == "simd_count" and int(val) > 0:
+                        n += 1
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def spawn_ranks(gpus: int, same_device: bool) -> None:
     """`bench.py --gpus N` (N > 1) outside torch.distributed.run: launch N ranks,
     one process per GPU, through torch.distributed.run as a CHILD process (this
-    process has not touched the GPU: device_count() does not initialise it) and
-    exit with its status.  Refuses to run on fewer than N visible GPUs."""
+    process never initialises HIP: the devices are counted from the environment /
+    KFD topology) and exit with its status.  Refuses to run on fewer than N
+    visible GPUs unless --same-device (every rank on GPU 0: the rank path's
+    rehearsal on a one-GPU box)."""
     import socket
     import subprocess
 
-    have = torch.cuda.device_count()
-    if have < gpus:
+    have = visible_gpus()
+    if have < (1 if same_device else gpus):
         print(f"bench.py: --gpus {gpus} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
         sys.exit(2)
     with socket.socket() as s:
@@ -351,6 +457,23 @@ def spawn_ranks(gpus: int) -> None:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
     sys.exit(subprocess.call(cmd, env=env))
+
+
+def gathered_parity(out, world, args, dev) -> bool:
+    """Outside the timed region: every rank's results gathered in rank order
+    (padded all-gather, unequal strong shards included) equal ONE launch over
+    the whole set on this GPU (regenerated from splitmix64 word 0)."""
+    allres = shd.gather_results(out, world)
+    if int(os.environ.get("RANK", "0")) != 0:
+        return True
+    total = args.strong_total if args.strong_total else world * args.blocks
+    whole = torch.empty(total * 4096, dtype=torch.uint8, device=dev)
+    jl.fill_random_dev(whole, SEED)
+    ref = jl.crc32c_fixed_dev(whole, 4096, total)
+    ok = bool(torch.equal(allres.to(ref.device), ref))
+    del whole, ref
+    torch.cuda.empty_cache()
+    return ok
 
 
 def main():
@@ -367,13 +490,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal of the N-rank path on one GPU: every rank on GPU 0, gloo collectives "
+                         "(the timing then measures N ranks sharing one GPU)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        spawn_ranks(args.gpus)
+        spawn_ranks(args.gpus, args.same_device)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the process group's size",
               file=sys.stderr, flush=True)
@@ -382,7 +508,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.same_device:  # RCCL refuses two ranks on one GPU: gloo carries the same collectives
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
     jl.init(local)
     stream = torch.cuda.current_stream()
@@ -428,7 +557,7 @@ def main():
         value = args.strong_total * 4096 * args.steps / wall / GIB
     else:
         value = shd.aggregate_rate(n * 4096, world, wall, args.steps)
-    gather_ms = None
+    gather_ms = parity = None
     if world > 1:  # result all-gather (unequal strong shards padded): reported beside, not part of the checksum path
         dist.barrier()
         torch.cuda.synchronize()
@@ -436,6 +565,7 @@ def main():
         shd.gather_results(out, world)
         torch.cuda.synchronize()
         gather_ms = shd.job_wall_time(time.perf_counter() - t0, dev) * 1e3
+        parity = gathered_parity(out, world, args, dev)
     alg_launch = n * (4096 + 4)
     achieved = alg_launch / (kern_ms / 1e3) / 1e9
     result = None
@@ -461,8 +591,10 @@ def main():
             "config": {"workload": (f"C4 strong: {args.strong_total} x 4 KiB blocks split over {world} GPUs"
                                     if args.strong_total else "C2: 1M x 4 KiB random blocks per GPU")
                        + ", masked CRC32C, device-resident",
-                       "blocks_per_gpu": n, "block_bytes": 4096, "parallelism": f"shard{world}"},
+                       "blocks_per_gpu": n, "block_bytes": 4096,
+                       "parallelism": f"shard{world}" + (" (same-device rehearsal, gloo)" if args.same_device else "")},
             "result_allgather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "parity_gathered_vs_single_launch": parity,
             "roofline": {
                 "bound": "hbm",
                 "kernel": "crc_fixed4k_v4_kernel<8 lanes/block, nt, 8-slot ring, 1024 threads>",
@@ -484,15 +616,15 @@ def main():
         if world == 1 and not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(data, n, gpu_out, args.cpu_seconds)
     if world == 1 and not args.no_secondary and not args.strong_total:  # secondaries describe the 1M-block C2 box
-        sec = [copy_inclusive_c2(data)]
+        sec = [copy_inclusive_c2(data), dispatch_latency()]
         sec[0]["parity_with_device_resident"] &= bool(np.array_equal(gpu_out, out.cpu().numpy().view(np.uint32)))
         del data
         torch.cuda.empty_cache()
         sec.append(secondary_c3(dev, stream, 5, 2, cpu=not args.no_cpu))
         torch.cuda.empty_cache()
-        sec.append(secondary_c5(dev, stream, 5, 2, cpu=not args.no_cpu))
-        torch.cuda.empty_cache()
-        sec.append(secondary_c5(dev, stream, 5, 2, mixed=True, cpu=not args.no_cpu))
+        for which in wl.C5_SETS:
+            sec.append(secondary_c5(dev, stream, 5, 2, which=which, cpu=not args.no_cpu))
+            torch.cuda.empty_cache()
         result["secondary"] = sec
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -93,6 +93,15 @@ const char *jl_version(void);
  *                            directly (the default), 0 = copy pageable input
  *                            through pinned staging buffers
  *   JL_OPT_STAGE_THREADS     host threads copying pageable input into staging (8)
+ *   JL_OPT_HOST_THRESHOLD    host-memory entry points jl_crc32c_fixed / _batch and
+ *                            jl_table_verify: a call touching fewer bytes than
+ *                            this runs on the calling thread's SSE4.2 path
+ *                            (bit-identical; no device work; a device must still
+ *                            be present); 0 = always the device.  Default 2 MiB,
+ *                            the measured crossover of the per-call latencies
+ *                            (one table)
+ *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
+ *                            default 12 MiB (one WAL)
  * Study builds only (make STUDY=1): JL_OPT_FIXED_KERNEL, JL_OPT_GV4_VARIANT. */
 #define JL_OPT_GENERAL_PATH 1
 #define JL_OPT_STREAM_DEPTH 2
@@ -100,6 +109,8 @@ const char *jl_version(void);
 #define JL_OPT_SPLIT_CAP 4
 #define JL_OPT_HOST_REGISTER 5
 #define JL_OPT_STAGE_THREADS 6
+#define JL_OPT_HOST_THRESHOLD 7
+#define JL_OPT_LOG_HOST_THRESHOLD 8
 #define JL_OPT_FIXED_KERNEL 100
 #define JL_OPT_GV4_VARIANT 101
 #define JL_PATH_AUTO 0
@@ -218,9 +229,11 @@ typedef struct jl_log_event {
  *   JL_LOG_NO_CHECKSUM     header walk only, every record accepted;
  *   JL_LOG_CHECKSUM        header walk kernel, then every OK record's crc range
  *                          cut into chunks of <= 4 KiB sorted into rounds of one
- *                          window count through the general v4 kernel (the
- *                          default; no host round trip before the final event
- *                          count);
+ *                          window count through the general v4 kernel; blocks of
+ *                          more than 64 records (DBBench's default 100-B values)
+ *                          are verified whole from a copy in LDS instead (the
+ *                          default; one pass for any log, no host round trip
+ *                          before the final event count);
  *   JL_LOG_CHECKSUM_TWO_PASS  the same path (explicit name);
  *   JL_LOG_CHECKSUM_FUSED  one pass over the bytes that walks and verifies
  *                          together (log_stream.hip); same results, slower on
@@ -235,12 +248,13 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
 /* Asynchronous form of jl_log_verify_dev (same path and events): returns once
  * the kernels are enqueued on `stream`; the result words land in device memory
  * d_result[3] in stream order: [0] the event total (events past `cap` are not
- * written), [1] blocks holding more than the walk's 64 event slots — when
- * non-zero the events are incomplete and the log must be verified again with
- * jl_log_verify_dev, which re-walks such blocks —, [2] non-zero if an internal
- * capacity was exceeded (likewise).  checksum: JL_LOG_NO_CHECKSUM,
+ * written: the events are complete when [0] <= cap, for any log), [1] the
+ * number of dense blocks (more than 64 records; informational), [2] non-zero if
+ * an internal capacity was exceeded (cannot happen; reported rather than
+ * assumed).  checksum: JL_LOG_NO_CHECKSUM,
  * JL_LOG_CHECKSUM or JL_LOG_CHECKSUM_TWO_PASS.  A thread's log calls share its
- * scratch: a call on another stream first waits for this one.  Lets a caller
+ * scratch: a later call on another stream (the null stream included) first makes
+ * its stream wait for this one (device-side).  Lets a caller
  * keep several verifications in flight back to back (no host round trip per
  * log); replaces the same readPhysicalRecord loop (J/db/LogReader.java:297-383). */
 int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,

@@ -209,7 +209,7 @@ def shutdown() -> None:
 
 
 OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 3, 4
-OPT_HOST_REGISTER, OPT_STAGE_THREADS = 5, 6
+OPT_HOST_REGISTER, OPT_STAGE_THREADS, OPT_HOST_THRESHOLD, OPT_LOG_HOST_THRESHOLD = 5, 6, 7, 8
 OPT_FIXED_KERNEL, OPT_GV4_VARIANT = 100, 101  # study builds only
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
 
@@ -239,6 +239,12 @@ def _dptr(t) -> int:
     return t.data_ptr()
 
 
+def _nbytes(t) -> int:
+    """Size in bytes of a device tensor (the arena / file bound the device range
+    checks use: numel() alone undercounts any dtype wider than a byte)."""
+    return t.numel() * t.element_size()
+
+
 def _stream(stream=None):
     import torch
 
@@ -251,8 +257,8 @@ def crc32c_fixed_dev(data, block_bytes: int, n_blocks: int | None = None, flags:
     """Per-block (masked) CRC32C of contiguous blocks in a uint8 device tensor."""
     import torch
 
-    n_blocks = data.numel() // block_bytes if n_blocks is None else n_blocks
-    if n_blocks * block_bytes > data.numel():
+    n_blocks = _nbytes(data) // block_bytes if n_blocks is None else n_blocks
+    if n_blocks * block_bytes > _nbytes(data):
         raise JLError("blocks exceed the tensor")
     if out is None:
         out = torch.empty(n_blocks, dtype=torch.int32, device=data.device)
@@ -281,7 +287,7 @@ def crc32c_batch_dev(base, off, length, init=None, suffix=None, flags: int = FLA
     n = off.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=base.device)
-    _check(lib().jl_crc32c_batch_dev(_dptr(base), base.numel(), _dptr(off), _dptr(length), _dptr(init), _dptr(suffix),
+    _check(lib().jl_crc32c_batch_dev(_dptr(base), _nbytes(base), _dptr(off), _dptr(length), _dptr(init), _dptr(suffix),
                                      n, flags,
                                      _dptr(out), _stream(stream)), "jl_crc32c_batch_dev")
     return out
@@ -352,7 +358,7 @@ def table_verify_dev(file, off, size, out=None, stream=None):
     n = off.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.uint8, device=file.device)
-    _check(lib().jl_table_verify_dev(_dptr(file), file.numel(), _dptr(off), _dptr(size), n, _dptr(out),
+    _check(lib().jl_table_verify_dev(_dptr(file), _nbytes(file), _dptr(off), _dptr(size), n, _dptr(out),
                                      _stream(stream)),
            "jl_table_verify_dev")
     return out
@@ -435,12 +441,12 @@ def log_verify_dev(log, checksum: bool = True, events=None, stream=None):
     import torch
 
     n = ctypes.c_uint64(0)
-    cap = 0 if events is None else events.numel() // LOG_EVENT_DTYPE.itemsize
-    rc = lib().jl_log_verify_dev(_dptr(log), log.numel(), int(checksum), _dptr(events), cap, ctypes.byref(n),
+    cap = 0 if events is None else _nbytes(events) // LOG_EVENT_DTYPE.itemsize
+    rc = lib().jl_log_verify_dev(_dptr(log), _nbytes(log), int(checksum), _dptr(events), cap, ctypes.byref(n),
                                  _stream(stream))
     if rc == -5:  # JL_ERR_CAPACITY: allocate and retry
         events = torch.empty(max(1, n.value) * LOG_EVENT_DTYPE.itemsize, dtype=torch.uint8, device=log.device)
-        rc = lib().jl_log_verify_dev(_dptr(log), log.numel(), int(checksum), _dptr(events), n.value, ctypes.byref(n),
+        rc = lib().jl_log_verify_dev(_dptr(log), _nbytes(log), int(checksum), _dptr(events), n.value, ctypes.byref(n),
                                      _stream(stream))
     _check(rc, "jl_log_verify_dev")
     return events, n.value
@@ -449,14 +455,15 @@ def log_verify_dev(log, checksum: bool = True, events=None, stream=None):
 def log_verify_dev_async(log, checksum: bool = True, events=None, result=None, stream=None):
     """Asynchronous device-resident verification (jl_log_verify_dev_async): enqueues
     the kernels and returns (events, result) at once; result (3 x int64 on the
-    device, filled in stream order) = [events, blocks past the walk's slots,
-    capacity flag] — when [1] or [2] is non-zero use log_verify_dev instead."""
+    device, filled in stream order) = [events, dense blocks (informational),
+    internal-capacity flag]; the events are complete for any log when [0] <= the
+    events capacity."""
     import torch
 
     if result is None:
         result = torch.empty(3, dtype=torch.int64, device=log.device)
-    cap = 0 if events is None else events.numel() // LOG_EVENT_DTYPE.itemsize
-    _check(lib().jl_log_verify_dev_async(_dptr(log), log.numel(), int(checksum), _dptr(events), cap, _dptr(result),
+    cap = 0 if events is None else _nbytes(events) // LOG_EVENT_DTYPE.itemsize
+    _check(lib().jl_log_verify_dev_async(_dptr(log), _nbytes(log), int(checksum), _dptr(events), cap, _dptr(result),
                                          _stream(stream)), "jl_log_verify_dev_async")
     return events, result
 

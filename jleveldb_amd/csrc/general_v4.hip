@@ -277,7 +277,10 @@ __device__ __forceinline__ uint32_t gv4_deal(uint32_t i, uint32_t w, uint32_t W,
 }
 
 // Prefetch cursor: walks the wave's rounds gv4_deal(i, w, ...) entry by entry.
-template <int MODE, bool DBG>
+// L2W (study variant 7): every round's bytes are read from a 1 MiB window at the
+// start of the arena instead (the same round table and addressing pattern, the
+// data L2-resident: the CRC math without the HBM stream).
+template <int MODE, bool DBG, bool L2W = false>
 struct GPF {
     uint32_t r, R, W;  // rounds (< 2^31)
     uint32_t i, w;     // r = gv4_deal(i, w, W, R)
@@ -315,7 +318,12 @@ struct GPF {
         const uint32_t rn = uni(gv4_deal(i + 1u, w, W, R));
         vec_next = A.desc && E > (uint32_t)JL_GV4_RING && (k == 0u || Eprev >= (uint32_t)JL_GV4_RING) && rn < R;
         if (vec_next) desc_issue(A, rn, q, (k + 1u) & 1u);
-        const uint64_t p = v.p, n = (uint64_t)K * 128u - (p & 127u) - v.d;
+        uint64_t p = v.p;
+        if constexpr (L2W) {
+            const uint64_t b0 = (uint64_t)(uintptr_t)A.P.base & ~(uint64_t)127;
+            p = b0 + ((p - b0) & ((1u << 20) - 1u));
+        }
+        const uint64_t n = (uint64_t)K * 128u - (p & 127u) - v.d;
         const uint64_t pa = p & ~(uint64_t)15;
         addr = (p & ~(uint64_t)127) + 16u * l;
         // side chunks (16-B aligned, each holding a byte of what is needed): lane 0 / 1 of the group
@@ -393,7 +401,10 @@ struct GPF {
 
 // VAR: 0 = default (nt ring loads), 1 = strict (vmcnt(0) before every ring use:
 // debugging), 2 = ring loads without nt (cache-policy study), 3 = whole 8-entry
-// fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study)
+// fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study),
+// 6 = no step math (the loads, ring and round bookkeeping with a plain XOR per
+// step: the memory side alone; results wrong), 7 = the data of every round from
+// an L2-resident 1 MiB window (the math side alone; results wrong)
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
@@ -427,7 +438,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     uint32_t zero_v;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
 
-    GPF<MODE, DBG> pf;
+    GPF<MODE, DBG, VAR == 7> pf;
     pf.init(A, ci, w, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
     // The ring lives in PINNED registers (JL_GV4_SLOTS, the two prefetched
     // round-descriptor sets JL_GV4_DQ0/1 just below it), above what the
@@ -619,7 +630,11 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                             lds_at(ldsG, JL_GADDR(gl.l1, x, 2u)));                                         \
     const uint32_t A3 = lds_at(ldsG, JL_GADDR(gl.l0, x, 3u));
 #define JL_XS4(R0, R1, R2, R3)                                                                             \
-    {                                                                                                      \
+    if constexpr (VAR == 6) {                                                                              \
+        asm volatile("v_xor_b32 %0, %0, " R0 "\n\tv_xor_b32 %1, %1, " R1 "\n\tv_xor_b32 %2, %2, " R2        \
+                     "\n\tv_xor_b32 %3, %3, " R3                                                            \
+                     : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));                                             \
+    } else {                                                                                               \
         JL_LK(x0, t0_, u0_) JL_LK(x1, t1_, u1_) JL_LK(x2, t2_, u2_) JL_LK(x3, t3_, u3_)                    \
         asm volatile("v_bitop3_b32 %0, %4, %5, " R0 " bitop3:0x96\n\t"                                   \
                      "v_bitop3_b32 %1, %6, %7, " R1 " bitop3:0x96\n\t"                                    \
@@ -709,7 +724,8 @@ template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
 #if JL_STUDY
     // study variants: 1 = vmcnt(0) before every ring use, 4 = address checks,
-    // 5 = per-entry path only, 3 = whole 8-entry fast turns, 2 = no nt policy
+    // 5 = per-entry path only, 3 = whole 8-entry fast turns, 2 = no nt policy,
+    // 6 = no step math (memory side), 7 = L2-resident data (math side)
     if (A.study) {
         const int v = A.study;
         if (v == 1)
@@ -723,6 +739,12 @@ hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_
                                A, zero);
         else if (v == 3)
             hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 6)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 6>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 7)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 7>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
                                A, zero);
         else
             hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,

@@ -4,6 +4,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -13,6 +14,7 @@
 
 #include "../../include/jlcrc.h"
 #include "crc_math.hpp"
+#include "host_paths.hpp"
 #include "jlcrc_kernels.hpp"
 
 #ifndef JL_STUDY
@@ -107,18 +109,27 @@ struct Slot {
 // a thread's first call; released when the thread exits or by jl_shutdown.
 struct Workspace {
     hipStream_t stream = nullptr;  // compute stream of the host-memory entry points
-    DevBuf ws_lc, ws_slot, ws_desc, ws_big, ws_part, ws_tmp;  // chunked log verify (log_chunks.hip)
+    DevBuf ws_lc, ws_slot, ws_desc, ws_big, ws_part, ws_tmp, ws_stash;  // chunked log verify (log_chunks.hip)
     DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
     // the chunked log verify's result words: coherent host memory the last kernel
     // writes directly (no D2H copy of them, the host polls the stream)
     uint64_t *h_res = nullptr;
-    hipStream_t async_st = nullptr;  // stream of the last jl_log_verify_dev_async still possibly in flight
+    // the last jl_log_verify_dev_async may still be in flight on async_st (NULL is
+    // a valid stream, HIP's null stream: `async_pending` says whether there is one);
+    // async_done is recorded on that stream after its launches
+    bool async_pending = false;
+    hipStream_t async_st = nullptr;
+    hipEvent_t async_done = nullptr;
     Slot slot[2];
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (async_pending) (void)hipEventSynchronize(async_done);
+        async_pending = false;
+        if (async_done) (void)hipEventDestroy(async_done);
+        async_done = nullptr;
         if (h_res) (void)hipHostFree(h_res);
         h_res = nullptr;
-        for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_ls, &ws_lsev})
+        for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_stash, &ws_ls, &ws_lsev})
             b->release();
         for (Slot &sl : slot) {
             if (sl.st) (void)hipStreamSynchronize(sl.st);
@@ -181,6 +192,7 @@ int get_ws(Workspace **out) {
     }
     Workspace &w = *t_ws.w;
     if (!w.stream) JL_HIP(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    if (!w.async_done) JL_HIP(hipEventCreateWithFlags(&w.async_done, hipEventDisableTiming));
     for (Slot &sl : w.slot) {
         if (!sl.st) JL_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
         if (!sl.copied) JL_HIP(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
@@ -189,6 +201,18 @@ int get_ws(Workspace **out) {
     *out = &w;
     return JL_OK;
 }
+
+// Host-memory calls touching fewer bytes than these run on the calling thread's
+// SSE4.2 path (host_paths.cpp): below them the device round trip (copies,
+// launches, synchronisation) costs more than the CRC itself.  Measured per-call
+// latencies (bench.py "dispatch", r3b; pageable input, one caller): a table of
+// ~4.2 KB blocks breaks even at 2 MiB (148 vs 145 us) and the device wins from
+// 4 MiB (227 vs 286 us); a WAL of 1 056-B records costs the device more (the
+// walk's ~12 launches): host 259 vs device 361 us at 4 MiB, 510 vs 658 at
+// 8 MiB, device ahead from 16 MiB (638 vs 803).  So the reference's own call
+// sizes — one <= 2 MiB table at open, one <= 4 MiB WAL at recovery — stay on
+// the host, batches of tables and large logs go to the device.
+constexpr int64_t kHostThresholdDefault = 2 << 20, kLogHostThresholdDefault = 12 << 20;
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
 // batch takes and its tuning.  Defaults are the measured best; tests force the
@@ -200,6 +224,8 @@ struct Options {
     int64_t split_cap = -1;           // JL_OPT_SPLIT_CAP: chunks of split blocks (-1: min(2^20, 2048 n))
     int host_register = 1;            // JL_OPT_HOST_REGISTER: pin pageable inputs >= 64 MiB for the call
     int stage_threads = 8;            // JL_OPT_STAGE_THREADS: host threads copying into pinned staging
+    int64_t host_threshold = kHostThresholdDefault;  // JL_OPT_HOST_THRESHOLD: smaller host-memory calls run on the host
+    int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
     int fixed_kernel = 7;             // study: JL_OPT_FIXED_KERNEL (7 = the v4 product kernel)
     int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
 };
@@ -253,12 +279,19 @@ struct HostSrc {
     HostSrc(const void *ptr, uint64_t n) : p((const uint8_t *)ptr), bytes(n) {
         PinRegistry &R = pin_registry();
         std::lock_guard<std::mutex> lk(R.mu);
-        for (PinRegistry::Pin &q : R.pins)  // inside a range another call of the engine pinned
-            if ((const uint8_t *)q.p <= p && p + bytes <= (const uint8_t *)q.p + q.bytes) {
+        for (PinRegistry::Pin &q : R.pins) {
+            const uint8_t *qa = (const uint8_t *)q.p, *qb = qa + q.bytes;
+            if (qa <= p && p + bytes <= qb) {  // inside a range another call of the engine pinned
                 q.refs++;
                 direct = shared = true;
                 return;
             }
+            // overlapping an engine pin without lying inside it: the pin may be
+            // dropped under this call's DMA (and hipPointerGetAttributes below
+            // would report the whole range as pinned from its start alone), and a
+            // second registration of the overlap fails: stage it
+            if (p < qb && qa < p + bytes) return;
+        }
         hipPointerAttribute_t attr;
         direct = hipPointerGetAttributes(&attr, ptr) == hipSuccess && attr.type == hipMemoryTypeHost;
         (void)hipGetLastError();  // pageable memory reports an error here; clear it
@@ -734,12 +767,20 @@ int jl_set_option(int option, int64_t value) {
         if (value < 1 || value > 64) break;
         o.stage_threads = (int)value;
         return JL_OK;
+    case JL_OPT_HOST_THRESHOLD:
+        if (value < 0) break;
+        o.host_threshold = value;
+        return JL_OK;
+    case JL_OPT_LOG_HOST_THRESHOLD:
+        if (value < 0) break;
+        o.log_host_threshold = value;
+        return JL_OK;
 #if JL_STUDY
     case JL_OPT_FIXED_KERNEL:
         o.fixed_kernel = (int)value;
         return JL_OK;
     case JL_OPT_GV4_VARIANT:
-        if (value < 0 || value > 5) break;
+        if (value < 0 || value > 7) break;
         o.gv4_variant = (int)value;
         return JL_OK;
 #endif
@@ -758,6 +799,8 @@ int64_t jl_get_option(int option) {
     case JL_OPT_SPLIT_CAP: return o.split_cap;
     case JL_OPT_HOST_REGISTER: return o.host_register;
     case JL_OPT_STAGE_THREADS: return o.stage_threads;
+    case JL_OPT_HOST_THRESHOLD: return o.host_threshold;
+    case JL_OPT_LOG_HOST_THRESHOLD: return o.log_host_threshold;
     case JL_OPT_FIXED_KERNEL: return o.fixed_kernel;
     case JL_OPT_GV4_VARIANT: return o.gv4_variant;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
@@ -890,6 +933,10 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     if (n_blocks == 0) return JL_OK;
     if (!host || !out || block_bytes == 0) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: bad arguments");
     if (block_bytes > JL_STREAM_CHUNK_BYTES) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: block larger than a chunk");
+    if ((int64_t)(n_blocks * block_bytes) < opt().host_threshold) {  // a small call: host SSE4.2 path
+        jlhost::fixed(host, block_bytes, n_blocks, flags, out);
+        return JL_OK;
+    }
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     const uint64_t per = JL_STREAM_CHUNK_BYTES / block_bytes;  // blocks per chunk
@@ -936,8 +983,16 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
     if (int r = ensure_ready()) return r;
     if (n == 0) return JL_OK;
     if (!base || !off || !len || !out) return fail(JL_ERR_INVALID, "jl_crc32c_batch: null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (off[i] + (uint64_t)len[i] > base_bytes) return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
+    uint64_t touched = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (off[i] > base_bytes || len[i] > base_bytes - off[i])
+            return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
+        touched += len[i];
+    }
+    if ((int64_t)touched < opt().host_threshold) {  // a small call: host SSE4.2 path
+        jlhost::batch(base, off, len, init, suffix, n, flags, out);
+        return JL_OK;
+    }
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     const std::vector<Chunk> ch = plan_chunks(off, len, 0, n);
@@ -1003,9 +1058,16 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
     if (int r = ensure_ready()) return r;
     if (n == 0) return JL_OK;
     if (!file || !off || !size || !status) return fail(JL_ERR_INVALID, "jl_table_verify: null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (off[i] + (uint64_t)size[i] + 5 > file_bytes)
+    uint64_t touched = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        if (off[i] > file_bytes || (uint64_t)size[i] + 5 > file_bytes - off[i])
             return fail(JL_ERR_INVALID, "jl_table_verify: truncated block read");  // TableFormat.java:203-206
+        touched += (uint64_t)size[i] + 5;
+    }
+    if ((int64_t)touched < opt().host_threshold) {  // a small call (one table): host SSE4.2 path
+        jlhost::table_verify(file, off, size, n, status);
+        return JL_OK;
+    }
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     const std::vector<Chunk> ch = plan_chunks(off, size, 5, n);  // block || 5-byte trailer
@@ -1130,38 +1192,46 @@ static int log_verify_stream(Workspace &c, const void *d_log, uint64_t log_bytes
     return JL_OK;
 }
 
-// Chunked log verification (log_chunks.hip): walk -> scans -> rounds setup ->
-// build -> crc_gv4_kernel<MODE_LOG_CHUNK> -> combine -> apply, stream-ordered,
-// one synchronisation at the end (the event count and the overflow flags).
-// The fast mode sizes the round table for at most kLCSlots events per 32 KiB
-// block (records of ~512 B and up); a log with a block of more events sets
-// *redo and the caller runs the exact mode, which reads the chunk totals back
-// after the walk and re-walks the blocks past their slots.
-// Waits for the stream's work by polling it (hipStreamQuery) instead of a
-// blocking synchronise.
+// Chunked log verification (log_chunks.hip): walk -> scans -> dense blocks ->
+// rounds setup -> build -> crc_gv4_kernel<MODE_LOG_CHUNK> -> combine -> apply,
+// stream-ordered, one pass for any log: the round table is sized for at most
+// kLCSlots events per 32 KiB block (records of ~500 B and up), and the blocks
+// of more events (dense) are verified whole by lc_dense instead.
+// Waits for the stream's work: polls it (hipStreamQuery) for up to kPollSpinUs,
+// then polls yielding the core to other threads up to kPollYieldUs, then blocks.
+// A log verification of a few MiB returns without the ~50 us wake-up of a
+// blocking synchronise (r2: 0.93 -> 0.88 ms on C5), and concurrent callers do
+// not each keep a host core spinning for long.
+constexpr double kPollSpinUs = 200.0, kPollYieldUs = 5000.0;
 static hipError_t poll_stream(hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         const hipError_t e = hipStreamQuery(st);
         if (e != hipErrorNotReady) return e;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (us > kPollYieldUs) return hipStreamSynchronize(st);
+        if (us > kPollSpinUs) std::this_thread::yield();
     }
 }
 
-// d_result null: synchronous (the count read back, *redo set when a block
-// overflowed its slots); else asynchronous: the result words go to d_result
-// on the stream and the call returns after the launches.
-static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum, int exact,
-                             jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st, bool *redo,
+// d_result null: synchronous (the count read back); else asynchronous: the
+// result words go to d_result on the stream and the call returns after the
+// launches.
+static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum,
+                             jl_log_event *d_events, uint64_t cap, uint64_t *n_events, hipStream_t st,
                              uint64_t *d_result = nullptr) {
-    *redo = false;
     if (log_bytes >= (1ull << 40)) return fail(JL_ERR_INVALID, "jl_log_verify: log larger than 1 TiB");
     const uint64_t nb = (log_bytes + 32767) / 32768, ng = (nb + jlk::kLCGroup - 1) / jlk::kLCGroup;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t hn = jlk::kLCCounters * ng + 1;
     const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
-                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_flag = o_fb + al(nb * 4),
-                 o_res = o_flag + 256, o_end = o_res + 256;
+                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
+                 o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_end = o_res + 256;
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
+    // the dense blocks' events: at most the caller's capacity (more events fail the call anyway)
+    const uint64_t stash_cap = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
+    JL_HIP(c.ws_stash.ensure(std::max<uint64_t>(stash_cap, 1) * 8));
     char *ws = (char *)c.ws_lc.p;
     jlk::LCArgs A;
     memset(&A, 0, sizeof(A));
@@ -1169,7 +1239,6 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.size = log_bytes;
     A.n_blocks = (uint32_t)nb;
     A.n_grp = (uint32_t)ng;
-    A.exact = exact;
     A.checksum = checksum ? 1 : 0;
     A.slots = (uint64_t *)c.ws_slot.p;
     A.count = (uint32_t *)(ws + o_cnt);
@@ -1178,13 +1247,20 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.hscan = (uint32_t *)(ws + o_hscan);
     A.rstart = (uint32_t *)(ws + o_rs);
     A.first_bad = (uint32_t *)(ws + o_fb);
+    A.dense_off = (uint64_t *)(ws + o_do);
     A.cap_flag = (uint32_t *)(ws + o_flag);
+    A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
+    A.stash = (uint64_t *)c.ws_stash.p;
+    A.stash_cap = stash_cap;
     if (!c.h_res) JL_HIP(hipHostMalloc((void **)&c.h_res, 64, hipHostMallocCoherent));
     A.result = d_result ? d_result : c.h_res;
     A.ev = (jlk::LogEvent *)d_events;
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
-    JL_HIP(jlk::launch_lc_walk(A, st));  // initialises count[nb], the hist tail, first_bad, cap_flag
+    // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
+    // dense blocks: verified whole, exact counts, events stashed (2 workgroups per CU)
+    JL_HIP(jlk::launch_lc_walk(A, st));
+    JL_HIP(jlk::launch_lc_dense(A, ctx().cus * 2, st));
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
     size_t t1 = 0, t2 = 0;
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, it, A.start, (int)(nb + 1), st));
@@ -1192,25 +1268,11 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     JL_HIP(c.ws_tmp.ensure(std::max(t1, t2)));
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t1, it, A.start, (int)(nb + 1), st));
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t2, A.hist, A.hscan, (int)hn, st));
-    // capacities of the round table, the multi-chunk records and their chunk states
-    uint64_t chunks, bigs, parts;
-    if (exact) {  // read the totals back
-        uint32_t h[3] = {0, 0, 0};
-        JL_HIP(hipMemcpyAsync(&h[0], A.hscan + jlk::kLCBig * ng, 4, hipMemcpyDeviceToHost, st));
-        JL_HIP(hipMemcpyAsync(&h[1], A.hscan + jlk::kLCPart * ng, 4, hipMemcpyDeviceToHost, st));
-        JL_HIP(hipMemcpyAsync(&h[2], A.hscan + jlk::kLCOver * ng, 4, hipMemcpyDeviceToHost, st));
-        JL_HIP(hipStreamSynchronize(st));
-        chunks = h[0];
-        bigs = h[1] - h[0];
-        parts = h[2] - h[1];
-    } else {  // <= kLCSlots records a block, and a block's bytes bound its extra chunks
-        chunks = nb * (jlk::kLCSlots + 10);
-        bigs = nb * 8;
-        parts = nb * 17;
-    }
-    A.round_cap = chunks / 8 + jlk::kLCBins + 1;
-    A.big_cap = bigs + 1;
-    A.part_cap = parts + 1;
+    // capacities of the round table, the multi-chunk records and their chunk states:
+    // <= kLCSlots records in a block that is not dense, and a block's bytes bound its extra chunks
+    A.round_cap = nb * (jlk::kLCSlots + 10) / 8 + jlk::kLCBins + 1;
+    A.big_cap = nb * 8 + 1;
+    A.part_cap = nb * 17 + 1;
     if (checksum) {
         JL_HIP(c.ws_desc.ensure(A.round_cap * 8 * sizeof(jlk::GDesc)));
         JL_HIP(c.ws_big.ensure(A.big_cap * sizeof(jlk::LCBig)));
@@ -1235,27 +1297,22 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         JL_HIP(jlk::launch_lc_apply(A, st));
     }
     if (d_result) return JL_OK;  // asynchronous: the caller reads d_result in stream order
-    // events, blocks past their slots, capacity flag (lc_finish, written to c.h_res
-    // by the last kernel): wait by polling the stream (a blocking synchronise
-    // sleeps, and a D2H copy of the words cost ~50 us between back-to-back calls)
+    // events, dense blocks, capacity flag (lc_finish, written to c.h_res by the
+    // last kernel): wait by polling the stream (a blocking synchronise sleeps,
+    // and a D2H copy of the words cost ~50 us between back-to-back calls)
     JL_HIP(poll_stream(st));
     const volatile uint64_t *hr = c.h_res;
     const uint64_t res[3] = {hr[0], hr[1], hr[2]};
-    if (res[1] && !exact) {
-        *redo = true;
-        return JL_OK;
-    }
     if (res[2]) return fail(JL_ERR_HIP, "jl_log_verify: internal capacity exceeded");
     *n_events = res[0];
     return JL_OK;
 }
 
-// Verifies d_log[0, log_bytes) on `st` with the calling thread's scratch `c`.
-// *n_events is known on return (the event count is read back); with sync_end
-// the events are complete too, else they complete in stream order (the host
-// pipeline copies them out on the same stream).
+// Verifies d_log[0, log_bytes) on `st` with the calling thread's scratch `c`;
+// *n_events is known on return (the event count is read back) and the events
+// are complete in stream order.
 static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events,
-                           uint64_t cap, uint64_t *n_events, hipStream_t st, bool sync_end) {
+                           uint64_t cap, uint64_t *n_events, hipStream_t st) {
     if (checksum == JL_LOG_CHECKSUM_FUSED) {  // the single-pass kernel, unless a block overflows its slots
         bool fallback = false;
         *n_events = 0;
@@ -1265,25 +1322,29 @@ static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, 
     }
     *n_events = 0;
     if (log_bytes == 0) return JL_OK;
-    int exact = 0;
-    for (;;) {
-        bool redo = false;
-        if (int r = log_verify_chunks(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, exact, d_events, cap, n_events,
-                                      st, &redo))
-            return r;
-        if (!redo) break;
-        exact = 1;  // a block held more than kLCSlots events: once more with exact sizing
-    }
+    if (int r = log_verify_chunks(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, n_events, st))
+        return r;
     if (*n_events > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
-    (void)sync_end;  // log_verify_chunks ends with a synchronisation (the event count)
     return JL_OK;
 }
 
 // The log-verify scratch of a workspace is reused by every call of its thread:
-// asynchronous calls left in flight on another stream are finished first.
-static int ws_order(Workspace &w, hipStream_t st, bool async) {
-    if (w.async_st && w.async_st != st) JL_HIP(hipStreamSynchronize(w.async_st));
-    w.async_st = async ? st : nullptr;
+// a call on another stream than an asynchronous call still possibly in flight
+// first makes its stream wait for that call's completion event (device-side,
+// no host wait).  Synchronous calls finish their work before they return.
+static int ws_order(Workspace &w, hipStream_t st) {
+    if (w.async_pending && w.async_st != st) JL_HIP(hipStreamWaitEvent(st, w.async_done, 0));
+    return JL_OK;
+}
+static int ws_after(Workspace &w, hipStream_t st, bool async, int rc) {
+    if (!async || rc) {
+        if (rc && w.async_pending) (void)hipEventSynchronize(w.async_done);
+        w.async_pending = false;
+        return rc;
+    }
+    JL_HIP(hipEventRecord(w.async_done, st));
+    w.async_pending = true;
+    w.async_st = st;
     return JL_OK;
 }
 
@@ -1295,8 +1356,8 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     const hipStream_t st = pick(stream);
-    if (int r = ws_order(*w, st, false)) return r;
-    return log_verify_impl(*w, d_log, log_bytes, checksum, d_events, cap, n_events, st, true);
+    if (int r = ws_order(*w, st)) return r;
+    return ws_after(*w, st, false, log_verify_impl(*w, d_log, log_bytes, checksum, d_events, cap, n_events, st));
 }
 
 int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
@@ -1308,15 +1369,15 @@ int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum,
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     const hipStream_t st = pick(stream);
-    if (int r = ws_order(*w, st, true)) return r;
+    if (int r = ws_order(*w, st)) return r;
     if (log_bytes == 0) {
         JL_HIP(hipMemsetAsync(d_result, 0, 3 * sizeof(uint64_t), st));
         return JL_OK;
     }
-    bool redo = false;
     uint64_t n = 0;
-    return log_verify_chunks(*w, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, 0, d_events, cap, &n, st, &redo,
-                             d_result);
+    return ws_after(*w, st, true,
+                    log_verify_chunks(*w, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, &n, st,
+                                      d_result));
 }
 
 // Host-memory log verification: chunks of JL_STREAM_CHUNK_BYTES (whole 32 KiB
@@ -1331,9 +1392,14 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     static_assert(JL_STREAM_CHUNK_BYTES % 32768 == 0, "log chunks must be whole blocks");
     *n_events = 0;
     if (log_bytes == 0) return JL_OK;
+    if ((int64_t)log_bytes < opt().log_host_threshold) {  // a small log (one WAL at recovery): host SSE4.2 path
+        jlhost::log_verify(log, log_bytes, checksum, events, cap, n_events);
+        if (*n_events > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+        return JL_OK;
+    }
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
-    if (int r = ws_order(*w, w->stream, false)) return r;
+    if (int r = ws_order(*w, w->stream)) return r;
     const uint64_t CH = JL_STREAM_CHUNK_BYTES, first = std::min(CH, log_bytes);
     const uint64_t ev_cap = first / 7 + 2;  // upper bound on a chunk's physical records
     for (Slot &sl : w->slot) {
@@ -1349,7 +1415,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
             uint64_t n = 0;
             jl_log_event *ev = (jl_log_event *)sl.d_out.p;
             if (int r = log_verify_impl(*w, sl.d_in.p, std::min(CH, log_bytes - i * CH), checksum, ev, ev_cap, &n,
-                                        w->stream, false))
+                                        w->stream))
                 return r;
             if (n && total + n <= cap) {  // past cap: keep counting for *n_events, copy nothing
                 JL_HIP(jlk::launch_event_rebase((jlk::LogEvent *)ev, n, i * CH, w->stream));
@@ -1359,6 +1425,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
             return JL_OK;
         });
     *n_events = total;
+    w->async_pending = false;  // the pipeline drained this thread's streams after any earlier async call
     if (rc) return rc;
     if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
     return JL_OK;

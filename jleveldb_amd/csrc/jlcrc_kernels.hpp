@@ -116,8 +116,16 @@ constexpr uint32_t kLCGroup = 64;        // 32 KiB blocks per walk group (one wa
 // z^-(4c) and z^-e tables (d = 16a + 4c + e), so its lookups are bank-conflict free
 constexpr uint32_t kLCBins = kLCWin * 16;
 constexpr uint32_t kLCBig = kLCBins, kLCPart = kLCBins + 1, kLCOver = kLCBins + 2;
-constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk records, parts, overflowing blocks
-constexpr uint32_t kLCSlots = 64;        // walked events kept per 32 KiB block
+constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk records, parts, dense blocks
+// walked events kept per 32 KiB block.  A block of more events, or whose first
+// kLCProbe events end within kLCProbe * 512 bytes (records of ~500 B and less),
+// is DENSE: lc_walk stops there (count = kLCDense), its chunks take no part in
+// the rounds, and lc_dense verifies it whole from a copy staged in LDS, writes
+// its exact event count and stashes its events (lc_build places them)
+constexpr uint32_t kLCSlots = 64;
+constexpr uint32_t kLCProbe = 8;
+constexpr uint32_t kLCDense = 0xffffffffu;  // count[b] of a dense block until lc_dense counts it
+constexpr uint32_t kLDMaxEv = 4688;         // >= events of one 32 KiB block (one per 7 bytes)
 constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
 struct LCBig {        // a record of more than one chunk
     uint64_t p;       // crc range start (h + 6) relative to the log
@@ -130,17 +138,24 @@ struct LCArgs {
     const uint8_t *log;
     uint64_t size;
     uint32_t n_blocks, n_grp;  // 32 KiB blocks, walk groups of kLCGroup blocks
-    int exact;             // 1: blocks with more than kLCSlots events are re-walked
     int checksum;
     uint64_t *slots;       // n_blocks * kLCSlots walked events: length | type << 16 | kind << 24 | stored << 32
-    uint32_t *count;       // n_blocks + 1 (count[n_blocks] = 0)
+    uint32_t *count;       // n_blocks + 1 (count[n_blocks] = 0); dense blocks: see kLCDense
+    // dense blocks' events, 8 B each (offset in block | length << 16 | type << 32 |
+    // kind << 40), block b's run at stash[dense_off[b]] (dense_off: kLCNotDense for
+    // the other blocks, written by lc_walk; ~0 for a dense block whose run did not
+    // fit: the caller's event array is too small anyway)
+    uint64_t *dense_off;
+    uint64_t *stash;
+    uint64_t stash_cap;
+    unsigned long long *stash_ctr;  // zeroed by lc_walk
     uint64_t *start;       // n_blocks + 1: exclusive scan of count
     uint32_t *hist;        // kLCCounters * n_grp + 1, counter-major (hist[c * n_grp + group])
     uint32_t *hscan;       // its exclusive scan
     uint32_t *rstart;      // kLCBins + 1: first round of every bin; [kLCBins] = rounds
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
     uint32_t *cap_flag;    // set when a capacity was exceeded
-    uint64_t *result;      // [0] events, [1] blocks past their slots, [2] cap_flag (written last)
+    uint64_t *result;      // [0] events, [1] dense blocks, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8
     uint64_t round_cap;    // rounds the desc array holds
     LCBig *big;
@@ -156,6 +171,8 @@ hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_dense(const LCArgs &A, int grid, hipStream_t st);
+constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
 
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)
 // inside the caller's base_bytes

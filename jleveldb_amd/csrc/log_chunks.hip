@@ -87,9 +87,23 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
     return (uint64_t)ld_u32u(p) | ((uint64_t)(ld_u32u(p + 3) >> 8) << 32);
 }
 
+// Adds one (s = 1) or removes one (s = ~0u) record of geometry g to the chunk
+// histogram of its walk group: its chunks by bin, plus one multi-chunk record
+// and its J parts when J > 1.
+__device__ __forceinline__ void lc_hist(uint32_t *h, const LCGeom &g, uint32_t s) {
+    if (g.J == 1u) {
+        atomicAdd(&h[lc_bin(g.K, g.r)], s);
+    } else {
+        atomicAdd(&h[lc_bin(kLCWin, 0u)], (g.J - 1u) * s);
+        atomicAdd(&h[lc_bin(g.K - kLCWin * (g.J - 1u), g.r)], s);
+        atomicAdd(&h[kLCBig], s);
+        atomicAdd(&h[kLCPart], g.J * s);
+    }
+}
+
 // Walk groups of kLCGroup consecutive blocks, one per wave (4 per workgroup).
 // The walk also initialises what later kernels accumulate into (first_bad,
-// count[n_blocks], the scan's zero tail, cap_flag): no memsets.
+// count[n_blocks], the scan's zero tail, cap_flag, the stash counter): no memsets.
 //
 // Latency: a block's headers form a chain of dependent loads, so the walk is
 // one DRAM round trip per record.  The first kLCLdsSlots events of a block are
@@ -108,6 +122,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         A.count[A.n_blocks] = 0;
         A.hist[(uint64_t)kLCCounters * A.n_grp] = 0;
         *A.cap_flag = 0;
+        *A.stash_ctr = 0;
     }
     uint32_t cnt = 0;
     if (b < A.n_blocks) {
@@ -117,35 +132,45 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         const uint64_t base = (uint64_t)(uintptr_t)A.log;
         uint64_t p = bs;
         uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
+        bool dense = false;
         for (;;) {
             const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
             if (d.kind == 0) break;  // the block's trailer: no event
+            // dense: a (kLCSlots + 1)-th event, or kLCProbe events within kLCProbe * 512 B
+            if (cnt == kLCSlots || (cnt == kLCProbe && p - bs < kLCProbe * 512u)) {
+                dense = true;
+                break;
+            }
             const uint64_t pn = p + 7u + d.length;
             const uint32_t stored = (uint32_t)hv;
             if (!d.stop && be - pn >= 7) hv = lc_header(A.log + pn, be - pn);
             const uint64_t slot = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
             if (cnt < kLCLdsSlots) ls[threadIdx.x][cnt] = slot;
-            else if (cnt < kLCSlots) A.slots[b * kLCSlots + cnt] = slot;
-            // chunk histogram: exactly the chunks lc_build places (in the fast
-            // mode only the kept events: a block that overflows its slots makes
-            // the caller run the exact mode)
-            if (d.kind == 1u && A.checksum && (cnt < kLCSlots || A.exact)) {
-                const LCGeom g = lc_geom(base + p + 6u, 1u + d.length);
-                if (g.J == 1u) {
-                    atomicAdd(&h[wv][lc_bin(g.K, g.r)], 1u);
-                } else {
-                    atomicAdd(&h[wv][lc_bin(kLCWin, 0u)], g.J - 1u);
-                    atomicAdd(&h[wv][lc_bin(g.K - kLCWin * (g.J - 1u), g.r)], 1u);
-                    atomicAdd(&h[wv][kLCBig], 1u);
-                    atomicAdd(&h[wv][kLCPart], g.J);
-                }
-            }
+            else A.slots[b * kLCSlots + cnt] = slot;
+            // chunk histogram: exactly the chunks lc_build places
+            if (d.kind == 1u && A.checksum) lc_hist(h[wv], lc_geom(base + p + 6u, 1u + d.length), 1u);
             cnt++;
             if (d.stop) break;
             p = pn;
         }
+        A.dense_off[b] = kLCNotDense;
+        if (dense) {
+            // lc_dense verifies the block and counts its events; the chunks of the
+            // events walked so far leave the histogram again (only blocks of short
+            // records take this second look at their slots)
+            if (A.checksum) {
+                uint64_t q = bs;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    const uint64_t s = j < kLCLdsSlots ? ls[threadIdx.x][j] : A.slots[b * kLCSlots + j];
+                    const uint32_t len = (uint32_t)s & 0xffffu;
+                    if ((((uint32_t)s >> 24) & 0xffu) == 1u) lc_hist(h[wv], lc_geom(base + q + 6u, 1u + len), ~0u);
+                    q += 7u + len;
+                }
+            }
+            atomicAdd(&h[wv][kLCOver], 1u);
+            cnt = kLCDense;
+        }
         A.count[b] = cnt;
-        if (cnt > kLCSlots) atomicAdd(&h[wv][kLCOver], 1u);
     }
     __syncthreads();
     // the LDS slots out, the workgroup's 256 blocks together: consecutive threads
@@ -211,48 +236,12 @@ __device__ __forceinline__ void lc_desc(const LCArgs &A, const uint32_t *rs, uin
     A.desc[round * 8u + rank % 8u] = g;
 }
 
-// The chunk descriptors of one OK record (ok false: none).  Ranks come from LDS
-// atomics per lane: with bins by (K, d mod 16) a wave's records spread over many
-// bins, so ballot aggregation would loop once per distinct bin.
-__device__ __forceinline__ void lc_place(const LCArgs &A, uint32_t *ctr, const uint32_t *rs, bool ok, uint64_t prel,
-                                         uint32_t n, uint32_t stored) {
-    if (!ok) return;
-    const LCGeom g = lc_geom((uint64_t)(uintptr_t)A.log + prel, n);
-    if (g.J == 1u) {
-        lc_desc(A, rs, g.K, atomicAdd(&ctr[lc_bin(g.K, g.r)], 1u), prel, 1u, g.r, 0u, stored);
-        return;
-    }
-    const uint32_t bi = atomicAdd(&ctr[kLCBig], 1u), pi = atomicAdd(&ctr[kLCPart], g.J);
-    // past a capacity (cannot happen with the caller's bounds) the chunks still
-    // take their ranks, as empty groups: no round of the table is left unwritten
-    const bool fits = bi < A.big_cap && (uint64_t)pi + g.J <= A.part_cap;
-    if (fits) {
-        LCBig big;
-        big.p = prel;
-        big.n = n;
-        big.stored = stored;
-        big.part0 = pi;
-        big.J = g.J;
-        A.big[bi] = big;
-    } else {
-        atomicOr(A.cap_flag, 1u);
-        if (bi < A.big_cap) A.big[bi].J = 0u;  // skipped by lc_combine
-    }
-    const uint64_t arel = prel - g.f;  // the record's first window (chunks j >= 1 start on the grid)
-    for (uint32_t j = 0; j < g.J; j++) {
-        const bool last = j + 1u == g.J;
-        const uint32_t K = last ? g.K - kLCWin * j : kLCWin;
-        const uint32_t d = last ? g.r : 0u;
-        const uint32_t rank = atomicAdd(&ctr[lc_bin(K, d)], 1u);
-        lc_desc(A, rs, K, rank, j ? arel + 4096ull * j : prel, j == 0u, d, fits ? kGPart | (pi + j) : kGNull,
-                0u);
-    }
-}
-
 __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v);
 
-// lc_place for a whole wave, one record per lane (ok false: none), all lanes
-// calling: a one-chunk record places its descriptor from its own lane; the
+// The chunk descriptors of one OK record per lane (ok false: none), all lanes
+// calling.  Ranks come from LDS atomics per lane: with bins by (K, d mod 16) a
+// wave's records spread over many bins, so ballot aggregation would loop once
+// per distinct bin.  A one-chunk record places its descriptor from its own lane; the
 // chunks of longer records are spread over the wave's lanes (lane c takes
 // chunk c of the wave's chunk list, its record found by a binary search over
 // the lanes' chunk offsets) instead of one lane placing its record's J chunks
@@ -372,18 +361,28 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
-        cnt[i] = b < A.n_blocks ? A.count[b] : 0u;
+        cnt[i] = b < A.n_blocks ? A.count[b] : 0u;  // dense blocks: counted by lc_dense
         st[i] = b < A.n_blocks ? A.start[b] : 0u;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
-        sl[i] = lane < cnt[i] ? A.slots[b * kLCSlots + lane] : 0ull;
+        sl[i] = lane < cnt[i] && cnt[i] <= kLCSlots ? A.slots[b * kLCSlots + lane] : 0ull;
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         if (b >= A.n_blocks) break;
+        const uint64_t doff = A.dense_off[b];
+        if (doff != kLCNotDense) {  // dense block: its events from the stash (lc_dense)
+            if (doff == ~0ull) continue;  // did not fit: the event array is too small anyway
+            for (uint32_t k = lane; k < cnt[i]; k += 64u) {
+                const uint64_t e = A.stash[doff + k];
+                lc_event(A, st[i] + k, b * 32768u + (e & 0xffffu), (uint32_t)(e >> 16) & 0xffffu,
+                         (uint32_t)(e >> 32) & 0xffu, (uint32_t)(e >> 40) & 0xffu);
+            }
+            continue;
+        }
         const uint64_t bs = b * 32768u, s = sl[i];
         const bool have = lane < cnt[i];  // lane < kLCSlots always
         const uint32_t length = (uint32_t)s & 0xffffu, type = ((uint32_t)s >> 16) & 0xffu, kind = (uint32_t)s >> 24;
@@ -391,23 +390,6 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         const uint64_t h = bs + lc_wave_excl_sum(have ? 7u + length : 0u);  // this event's header
         if (have) lc_event(A, st[i] + lane, h, length, type, kind);
         if (A.checksum) lc_place_wave(A, ctr, rs, have && kind == 1u, h + 6u, 1u + length, stored);
-        if (cnt[i] <= kLCSlots || !A.exact) continue;
-        // exact mode: the events past the slots (a block of many short records)
-        // are walked again by lane 0 from the header after the last kept one (an
-        // OK record: only OK records continue the walk)
-        uint64_t p = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)h, (int)(kLCSlots - 1u)) |
-                     ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(h >> 32), (int)(kLCSlots - 1u)) << 32);
-        p += 7u + (uint32_t)__builtin_amdgcn_readlane((int)length, (int)(kLCSlots - 1u));
-        const uint64_t be = bs + 32768u < A.size ? bs + 32768u : A.size;
-        const bool eof = be - bs < 32768u;
-        for (uint32_t j = kLCSlots; j < cnt[i]; j++) {
-            const uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
-            const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
-            if (lane == 0u) lc_event(A, st[i] + j, p, d.length, d.type, d.kind);
-            if (A.checksum) lc_place(A, ctr, rs, lane == 0u && d.kind == 1u, p + 6u, 1u + d.length, (uint32_t)hv);
-            if (d.stop) break;
-            p += 7u + d.length;
-        }
     }
     if (!A.checksum) lc_finish(A);  // the last kernel of a walk-only verification
 }
@@ -464,6 +446,191 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
             else if (off > f) A.ev[i].kind = 0u;  // dropped with the rest of the block
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Dense blocks (lc_walk's kLCDense: records of ~500 B and less, e.g. DBBench's
+// default 100-B values make ~237 records of 138 B per 32 KiB block).  Cutting
+// them into 8-chunk rounds would pay a round epilogue per ~2 windows, so a
+// workgroup takes the whole block instead: it stages the block in LDS, walks
+// its headers there, checks every record's crc with one thread per record
+// (slicing-by-4 from LDS tables) and stashes the block's events in file order
+// (8 B each) with its exact event count, before the event scan; lc_build copies
+// them to their places.  Persistent grid over the blocks lc_walk marked; each
+// workgroup loads its next dense block into registers while it works on the
+// current one.
+//
+// The walk (one wave) speculates: after a header of length n, lane k reads the
+// header at p + k (7 + n); the lanes up to the first one that is not an OK
+// record of the same length are the next headers of the chain (the reference's
+// decisions in its order, J/db/LogReader.java:297-383), so a run of equal
+// records is walked 64 headers per LDS round trip; unequal lengths advance one
+// header per round.
+//
+// Tables: kLDRep copies of T0..T3 interleaved so that copy r sits in banks
+// {r, r + kLDRep, ...} and thread t reads copy t mod kLDRep: the random lookups
+// of 32 lanes conflict only among the 32 / kLDRep lanes sharing a copy.
+__device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
+    return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
+}
+
+#ifndef JL_LD_REP
+#define JL_LD_REP 4
+#endif
+constexpr uint32_t kLDThreads = 256, kLDRep = JL_LD_REP;
+// A workgroup's dense blocks: the candidates blockIdx.x + j * gridDim.x, 64 of
+// them per wave-wide load of count[] (the ballot of the dense ones is kept, so a
+// log of dense blocks costs one load per 64 blocks and a log without any costs
+// n_blocks / (64 grid) loads per workgroup).
+struct LDSched {
+    uint64_t base, mask;
+    uint32_t step;
+    __device__ __forceinline__ uint64_t scan(const LCArgs &A) const {
+        const uint64_t i = base + (uint64_t)(threadIdx.x & 63u) * step;
+        return __builtin_amdgcn_ballot_w64(i < A.n_blocks && A.count[i] == kLCDense);
+    }
+    __device__ __forceinline__ void init(const LCArgs &A) {
+        step = gridDim.x;
+        base = blockIdx.x;
+        mask = scan(A);
+    }
+    __device__ __forceinline__ uint64_t next(const LCArgs &A) {  // n_blocks when done
+        while (!mask) {
+            base += 64ull * step;
+            if (base >= A.n_blocks) return A.n_blocks;
+            mask = scan(A);
+        }
+        const uint32_t j = (uint32_t)__builtin_ctzll(mask);
+        mask &= mask - 1u;
+        return base + (uint64_t)j * step;
+    }
+};
+// a block can be loaded with whole 16-B vector loads (full, 16-B aligned)
+__device__ __forceinline__ bool ld_vec(const LCArgs &A, uint64_t b) {
+    return b < A.n_blocks && A.size - b * 32768u >= 32768u && ((uintptr_t)(A.log + b * 32768u) & 15u) == 0;
+}
+
+__global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
+    __shared__ uint32_t dat[8192 + 4];          // the block (+ zero pad: header reads near its end)
+    __shared__ uint32_t tab[4 * 256 * kLDRep];  // T_k[e] copy r at word (256 k + e) kLDRep + r
+    __shared__ uint16_t hl[kLDMaxEv];           // header offsets of the block's events
+    __shared__ uint32_t s_n, s_bad;
+    __shared__ unsigned long long s_off;
+    const uint32_t t = threadIdx.x, lane = t & 63u, rep = t % kLDRep;
+    {  // T0 from aux (crc_math.hpp build_aux), T_k[e] = T_{k-1}[e] >> 8 ^ T0[T_{k-1}[e] & 0xff]
+        uint32_t v = A.aux[t];
+        for (uint32_t r = 0; r < kLDRep; r++) tab[t * kLDRep + r] = v;
+        for (uint32_t k = 1; k < 4; k++) {
+            v = (v >> 8) ^ A.aux[v & 0xffu];
+            for (uint32_t r = 0; r < kLDRep; r++) tab[(256u * k + t) * kLDRep + r] = v;
+        }
+    }
+    const uint32_t *T = tab + rep;
+    const uint8_t *by = (const uint8_t *)dat;
+    LDSched sch;
+    sch.init(A);
+    uint64_t b = sch.next(A);
+    uint4 pre[8];
+    if (ld_vec(A, b))
+#pragma unroll
+        for (uint32_t k = 0; k < 8; k++) pre[k] = ((const uint4 *)(A.log + b * 32768u))[k * kLDThreads + t];
+    while (b < A.n_blocks) {
+        const uint64_t bs = b * 32768u;
+        const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+        const bool eof = blen < 32768u;
+        __syncthreads();  // the previous block's readers of dat / hl / s_* are done
+        if (ld_vec(A, b)) {
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) ((uint4 *)dat)[k * kLDThreads + t] = pre[k];
+        } else {  // the file's short last block (or an unaligned log): bytes, nothing past its end
+            const uint8_t *src = A.log + bs;
+            for (uint32_t o = t; o < 8192u; o += kLDThreads) {
+                uint32_t v = 0;
+                for (uint32_t j = 0; j < 4; j++)
+                    if (4u * o + j < blen) v |= (uint32_t)src[4u * o + j] << (8 * j);
+                dat[o] = v;
+            }
+        }
+        if (t < 4) dat[8192 + t] = 0;
+        __syncthreads();
+        const uint64_t bn = sch.next(A);  // its bytes load during this block's work
+        if (ld_vec(A, bn))
+#pragma unroll
+            for (uint32_t k = 0; k < 8; k++) pre[k] = ((const uint4 *)(A.log + bn * 32768u))[k * kLDThreads + t];
+        unsigned long long off = 0;
+        if (t < 64) {  // the walk, wave 0
+            uint32_t p = 0, n = 0;
+            for (;;) {
+                const uint32_t rem = blen - p;
+                const LCDecision d0 = lc_decide(rem, eof, rem >= 7 ? lds32u(dat, p + 3u) : 0u);
+                if (d0.kind == 0) break;  // the block's trailer: no event
+                if (d0.stop) {
+                    if (lane == 0) hl[n] = (uint16_t)p;
+                    n++;
+                    break;
+                }
+                const uint32_t L = 7u + d0.length, cand = p + lane * L;
+                bool ok = lane == 0;
+                if (lane && cand < blen && blen - cand >= 7) {
+                    const LCDecision dk = lc_decide(blen - cand, eof, lds32u(dat, cand + 3u));
+                    ok = dk.kind == 1u && dk.length == d0.length;
+                }
+                const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
+                const uint32_t m = nok ? (uint32_t)__builtin_ctzll(nok) : 64u;
+                if (lane < m) hl[n + lane] = (uint16_t)cand;
+                n += m;
+                p += m * L;
+            }
+            if (lane == 0) {
+                s_n = n;
+                s_bad = kLCNone;
+                off = atomicAdd(A.stash_ctr, (unsigned long long)n);  // used after the crcs: its latency hides
+            }
+        }
+        __syncthreads();
+        const uint32_t n = s_n;
+        if (A.checksum) {  // one thread per OK record: crc over type || payload (J/db/LogWriter.java:147)
+            for (uint32_t r = t; r < n; r += kLDThreads) {
+                const uint32_t h = hl[r];
+                const LCDecision d = lc_decide(blen - h, eof, lds32u(dat, h + 3u));
+                if (d.kind != 1u) continue;
+                const uint32_t e = h + 7u + d.length;
+                uint32_t x = 0xffffffffu, q = h + 6u;
+                for (; q < e && (q & 3u); q++) x = (x >> 8) ^ T[((x ^ by[q]) & 0xffu) * kLDRep];
+                for (; q + 4u <= e; q += 4u) {
+                    x ^= dat[q >> 2];
+                    x = xor3(T[(768u + (x & 0xffu)) * kLDRep], T[(512u + ((x >> 8) & 0xffu)) * kLDRep],
+                             T[(256u + ((x >> 16) & 0xffu)) * kLDRep]) ^
+                        T[(x >> 24) * kLDRep];
+                }
+                for (; q < e; q++) x = (x >> 8) ^ T[((x ^ by[q]) & 0xffu) * kLDRep];
+                if (mask_crc(~x) != lds32u(dat, h)) atomicMin(&s_bad, r);
+            }
+        }
+        if (t == 0) {
+            s_off = off + n <= A.stash_cap ? off : ~0ull;  // past the stash: the caller's cap is short
+            A.count[b] = n;
+            A.dense_off[b] = s_off;
+        }
+        __syncthreads();
+        // the events in file order (8 B each); the first failing record is BAD_CRC
+        // and the rest of the block is dropped (J/db/LogReader.java:359-367)
+        const uint32_t bad = s_bad;
+        const unsigned long long so = s_off;
+        if (so != ~0ull)
+            for (uint32_t r = t; r < n; r += kLDThreads) {
+                const uint32_t h = hl[r];
+                const LCDecision d = lc_decide(blen - h, eof, blen - h >= 7 ? lds32u(dat, h + 3u) : 0u);
+                const uint64_t kind = r == bad ? 2u : (bad != kLCNone && r > bad ? 0u : d.kind);
+                A.stash[so + r] = h | ((uint64_t)d.length << 16) | ((uint64_t)d.type << 32) | (kind << 40);
+            }
+        b = bn;
+    }
+}
+
+hipError_t launch_lc_dense(const LCArgs &A, int grid, hipStream_t st) {
+    hipLaunchKernelGGL(lc_dense_kernel, dim3(grid), dim3(kLDThreads), 0, st, A);
+    return hipGetLastError();
 }
 
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {

@@ -3,6 +3,7 @@
 // readPhysicalRecord (:356-369) happened on the GPU; this replays the reader's
 // buffer bookkeeping, fragment reassembly, initial-offset handling and
 // Reporter calls exactly as the reference orders them.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <string>
@@ -106,9 +107,16 @@ extern "C" int jl_log_read_records(const uint8_t *log, uint64_t log_bytes, int c
     *n_reports = 0;
     std::vector<jl_log_event> ev;
     if (log_bytes) {
-        ev.resize(log_bytes / 7 + 2);
+        // events for records of ~256 B and up (16 B of events per 256 B of log);
+        // a denser log reports its event count and is verified once more into
+        // an array of that size (r2 sized for 7-B records: 2.3x the log)
+        ev.resize(std::min<uint64_t>(log_bytes / 7 + 2, log_bytes / 256 + 1024));
         uint64_t n_ev = 0;
         int r = jl_log_verify(log, log_bytes, checksum, ev.data(), ev.size(), &n_ev);
+        if (r == JL_ERR_CAPACITY && n_ev > ev.size()) {
+            ev.resize(n_ev);
+            r = jl_log_verify(log, log_bytes, checksum, ev.data(), ev.size(), &n_ev);
+        }
         if (r) return r;
         ev.resize(n_ev);
     }

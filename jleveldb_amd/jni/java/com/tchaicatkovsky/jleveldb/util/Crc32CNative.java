@@ -25,6 +25,16 @@ public final class Crc32CNative {
 
     public static native String lastError();
 
+    /** jl_set_option / jl_get_option (include/jlcrc.h JL_OPT_*); 0 or a negative error code. */
+    public static native int setOption(int option, long value);
+
+    public static native long getOption(int option);
+
+    /** Host-memory calls touching fewer bytes run on the host's SSE4.2 path (tables, batches). */
+    public static final int OPT_HOST_THRESHOLD = 7;
+    /** The same for log verification. */
+    public static final int OPT_LOG_HOST_THRESHOLD = 8;
+
     /** TableFormat.readBlock checksum test for many handles of one mmap'd table. */
     public static native int tableVerify(ByteBuffer file, long[] offset, int[] size, byte[] status);
 
@@ -36,6 +46,10 @@ public final class Crc32CNative {
      */
     public static native long tableBlockHandles(ByteBuffer file, long[] offset, int[] size, byte[] kind);
 
-    /** LogReader verification of a whole log image; returns the number of 16-byte events. */
+    /**
+     * LogReader verification of a whole log image; returns the number of 16-byte
+     * events (greater than events.capacity() / 16: grow the buffer and call
+     * again) or a negative error code.
+     */
     public static native long logVerify(ByteBuffer log, boolean checksum, ByteBuffer events);
 }

@@ -23,6 +23,17 @@ public final class Crc32CShims {
     static {
         int rc = Crc32CNative.init(0);
         if (rc != 0) throw new IllegalStateException("jlcrc: " + Crc32CNative.lastError());
+        // the call-size dispatch (DESIGN.md §1.3): a table or log smaller than the
+        // threshold is verified on the host's SSE4.2 path inside the engine; the
+        // defaults keep one <= 2 MiB table and one <= 4 MiB WAL on the host
+        setThreshold(Crc32CNative.OPT_HOST_THRESHOLD, "jlcrc.hostThreshold");
+        setThreshold(Crc32CNative.OPT_LOG_HOST_THRESHOLD, "jlcrc.logHostThreshold");
+    }
+
+    private static void setThreshold(int option, String property) {
+        String v = System.getProperty(property);
+        if (v != null && Crc32CNative.setOption(option, Long.parseLong(v)) != 0)
+            throw new IllegalArgumentException("jlcrc: " + property + "=" + v + ": " + Crc32CNative.lastError());
     }
 
     private static void putLE32(byte[] b, int off, long v) {
@@ -125,8 +136,19 @@ public final class Crc32CShims {
      */
     public static LogEvent[] verifyLog(ByteBuffer mappedLog, boolean checksum) {
         long size = mappedLog.capacity();
-        ByteBuffer events = ByteBuffer.allocateDirect((int) (16 * (size / 7 + 2))).order(ByteOrder.LITTLE_ENDIAN);
+        // one event per physical record: at most one per 7 bytes, but a direct
+        // buffer holds < 2 GiB, so start from a typical density and grow to the
+        // exact count the engine reports (JL_ERR_CAPACITY comes back with it)
+        long cap = Math.min(size / 7 + 2, (Integer.MAX_VALUE - 15) / 16);
+        cap = Math.min(cap, Math.max(1024, size / 512));
+        ByteBuffer events = ByteBuffer.allocateDirect((int) (16 * cap)).order(ByteOrder.LITTLE_ENDIAN);
         long n = Crc32CNative.logVerify(mappedLog, checksum, events);
+        if (n > cap) {  // more events than the buffer holds: the count came back, grow once
+            if (16 * n > Integer.MAX_VALUE)
+                throw new IllegalStateException("jlcrc: " + n + " log events exceed one direct buffer");
+            events = ByteBuffer.allocateDirect((int) (16 * n)).order(ByteOrder.LITTLE_ENDIAN);
+            n = Crc32CNative.logVerify(mappedLog, checksum, events);
+        }
         if (n < 0) throw new IllegalStateException("jlcrc: " + Crc32CNative.lastError());
         LogEvent[] out = new LogEvent[(int) n];
         for (int i = 0; i < n; i++) {

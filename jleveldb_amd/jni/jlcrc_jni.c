@@ -70,6 +70,18 @@ JNIEXPORT jint JNICALL JFN(init)(JNIEnv *env, jclass cls, jint device) {
     return jl_init(device);
 }
 
+/* jl_set_option: the call-size dispatch thresholds (JL_OPT_HOST_THRESHOLD,
+ * JL_OPT_LOG_HOST_THRESHOLD) and the other engine options */
+JNIEXPORT jint JNICALL JFN(setOption)(JNIEnv *env, jclass cls, jint option, jlong value) {
+    (void)env; (void)cls;
+    return jl_set_option(option, (int64_t)value);
+}
+
+JNIEXPORT jlong JNICALL JFN(getOption)(JNIEnv *env, jclass cls, jint option) {
+    (void)env; (void)cls;
+    return (jlong)jl_get_option(option);
+}
+
 JNIEXPORT jstring JNICALL JFN(lastError)(JNIEnv *env, jclass cls) {
     (void)cls;
     return (*env)->NewStringUTF(env, jl_last_error());
@@ -141,7 +153,9 @@ JNIEXPORT jlong JNICALL JFN(tableBlockHandles)(JNIEnv *env, jclass cls, jobject 
 
 /* Batched LogReader verification of a whole .log / MANIFEST image (direct
  * ByteBuffer): fills events as 16-byte jl_log_event records into `events`
- * (a direct ByteBuffer); returns the event count or a negative error. */
+ * (a direct ByteBuffer); returns the event count — larger than the buffer holds
+ * when it is too small (nothing usable was written: grow it to the count and
+ * call again, as for tableBlockHandles) — or a negative error. */
 JNIEXPORT jlong JNICALL JFN(logVerify)(JNIEnv *env, jclass cls, jobject log, jboolean checksum, jobject events) {
     (void)cls;
     uint8_t *l = (*env)->GetDirectBufferAddress(env, log);
@@ -154,5 +168,5 @@ JNIEXPORT jlong JNICALL JFN(logVerify)(JNIEnv *env, jclass cls, jobject log, jbo
     }
     uint64_t n = 0;
     int r = jl_log_verify(l, (uint64_t)bytes, checksum ? 1 : 0, ev, (uint64_t)evcap, &n);
-    return r ? (jlong)r : (jlong)n;
+    return (r == JL_OK || r == JL_ERR_CAPACITY) ? (jlong)n : (jlong)r;
 }

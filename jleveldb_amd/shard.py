@@ -136,6 +136,14 @@ def _pg_world() -> int:
     return dist.get_world_size()
 
 
+def _coll_device(device):
+    """Where a collective's tensors live: the caller's device under RCCL (nccl),
+    the host under gloo (CPU jobs, and bench.py --same-device)."""
+    import torch.distributed as dist
+
+    return "cpu" if dist.get_backend() == "gloo" else device
+
+
 def job_wall_time(local_seconds: float, device=None) -> float:
     """Max over ranks of the timed region (a no-op without a process group)."""
     import torch
@@ -143,7 +151,7 @@ def job_wall_time(local_seconds: float, device=None) -> float:
 
     if _pg_world() == 1:
         return float(local_seconds)
-    t = torch.tensor([float(local_seconds)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(local_seconds)], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -156,7 +164,7 @@ def total_mismatches(local_count: int, device=None) -> int:
 
     if _pg_world() == 1:
         return int(local_count)
-    t = torch.tensor([int(local_count)], dtype=torch.int64, device=device)
+    t = torch.tensor([int(local_count)], dtype=torch.int64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
 
@@ -178,16 +186,17 @@ def gather_results(local, world: int | None = None):
     world = _pg_world() if world is None else world
     if world == 1:
         return local
-    flat = local.reshape(-1)
+    home = local.device
+    flat = local.reshape(-1).to(_coll_device(home))
     n = torch.tensor([flat.numel()], dtype=torch.int64, device=flat.device)
     ns = [torch.empty_like(n) for _ in range(world)]
     dist.all_gather(ns, n)
     counts = [int(x.item()) for x in ns]
     cap = max(counts)
     if cap == 0:
-        return flat[:0]
+        return flat[:0].to(home)
     pad = torch.zeros(cap, dtype=flat.dtype, device=flat.device)
     pad[: flat.numel()] = flat
     parts = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(parts, pad)
-    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+    return torch.cat([p[:c] for p, c in zip(parts, counts)]).to(home)

@@ -13,6 +13,10 @@ SEED = 0x4A4C4442
 LOG_BLOCK = 32768  # J/db/LogFormat.java:52
 C5_LOG_BYTES = (1 << 17) * LOG_BLOCK  # 2^17 x 32 KiB = 4 GiB
 C1_PAYLOAD = 12 + 1 + 1 + 16 + 2 + 1024  # WriteBatch header + tag + varint + 16-B key + varint + 1 KiB value
+# DBBench's default write (J/benchmark/DBBench.java:80 FLAGS_value_size = 100, 16-B keys):
+# one Put per WriteBatch = 12-B header + tag + varint + 16-B key + varint + 100-B value
+DBBENCH_PAYLOAD = 12 + 1 + 1 + 16 + 1 + 100
+C5_SETS = ("c1_1056", "mixed_1b_100k", "dbbench_131")
 
 
 def c3_lengths(n: int = 1 << 20, seed: int = SEED) -> np.ndarray:
@@ -42,12 +46,18 @@ def _frag_bytes(lens: np.ndarray) -> np.ndarray:
     return lens + 7 * (lens // (LOG_BLOCK - 7) + 1)
 
 
-def c5_lengths(mixed: bool, target: int = C5_LOG_BYTES, seed: int = SEED) -> np.ndarray:
+def c5_lengths(mixed, target: int = C5_LOG_BYTES, seed: int = SEED) -> np.ndarray:
     """Config C5 payload lengths whose LogWriter framing fills about `target`
-    bytes: either C1-shaped records (1 056-B payloads) or a mixed 1 B - 100 KiB
-    set whose records fragment FIRST/MIDDLE/LAST across 32 KiB blocks."""
-    if not mixed:
+    bytes.  `mixed` names the set (C5_SETS; a bool picks the first two): C1-shaped
+    records (1 056-B payloads), a mixed 1 B - 100 KiB set whose records fragment
+    FIRST/MIDDLE/LAST across 32 KiB blocks, or DBBench-default records (131-B
+    payloads, ~237 per 32 KiB block: every block dense)."""
+    name = mixed if isinstance(mixed, str) else C5_SETS[1 if mixed else 0]
+    if name == "dbbench_131":
+        return np.full(target // (DBBENCH_PAYLOAD + 7), DBBENCH_PAYLOAD, np.uint32)
+    if name == "c1_1056":
         return np.full(target // (C1_PAYLOAD + 7), C1_PAYLOAD, np.uint32)
+    assert name == "mixed_1b_100k", name
     rng = np.random.default_rng(seed + 7)
     lens = rng.integers(1, 100 * 1024 + 1, target // (50 * 1024) + 1).astype(np.uint32)
     keep = int(np.searchsorted(np.cumsum(_frag_bytes(lens)), target))

@@ -7,7 +7,12 @@ whole-table verification.  Follows:
 
   BlockBuilder.add / finish        J/table/BlockBuilder.java:69-114
   TableBuilder.add / flush / finish / writeBlock / writeRawBlock
-                                   J/table/TableBuilder.java:130-186, 188-245, 269-323
+                                   J/table/TableBuilder.java:127-186, 188-245, 269-323
+  index keys: findShortestSeparator / findShortSuccessor of the table's comparator,
+    bytewise  J/util/BytewiseComparatorImpl.java:60-94
+    internal  J/db/format/InternalKeyComparator.java:77-109 (user key shortened,
+              then the tag packSequenceAndType(kMaxSequenceNumber, kValueTypeForSeek),
+              J/db/format/DBFormat.java:74-76,97-100)
   BlockHandle.encodeTo / decodeFrom J/table/TableFormat.java:66-78
   Footer.encodeTo / decodeFrom     J/table/TableFormat.java:116-146  (magic :161)
   Block (restart array) / decodeEntry  J/table/Block.java:44-84, 312-342
@@ -18,7 +23,9 @@ whole-table verification.  Follows:
 (J = src/main/java/com/tchaicatkovsky/jleveldb in the reference.)  The
 reference is Java and no JVM exists here, so the images are produced by this
 restatement; the walker parity is therefore pinned to the restated format, not
-to files written by the reference.
+to files written by the reference.  For a given key/value
+sequence, options (block size, restart interval, comparator) and filter block,
+the image is byte for byte what TableBuilder writes, index keys included.
 """
 from __future__ import annotations
 
@@ -50,6 +57,56 @@ def get_varint(buf: bytes, pos: int, limit: int) -> tuple[int, int]:
             return v, pos
         shift += 7
     raise ValueError("bad varint")
+
+
+K_MAX_SEQUENCE = (2**63 - 1) >> 8  # DBFormat.kMaxSequenceNumber = Long.MAX_VALUE >> 8 (DBFormat.java:76)
+SEEK_TAG = struct.pack("<Q", (K_MAX_SEQUENCE << 8) | 1)  # packSequenceAndType(.., kValueTypeForSeek = Value)
+
+
+def bytewise_shortest_separator(start: bytes, limit: bytes) -> bytes:
+    """BytewiseComparatorImpl.findShortestSeparator (:60-79)."""
+    m = min(len(start), len(limit))
+    i = 0
+    while i < m and start[i] == limit[i]:
+        i += 1
+    if i >= m:
+        return start  # one is a prefix of the other: not shortened
+    b = start[i]
+    if b < 0xFF and b + 1 < limit[i]:
+        return start[:i] + bytes([b + 1])
+    return start
+
+
+def bytewise_short_successor(key: bytes) -> bytes:
+    """BytewiseComparatorImpl.findShortSuccessor (:82-94)."""
+    for i, b in enumerate(key):
+        if b != 0xFF:
+            return key[:i] + bytes([b + 1])
+    return key  # a run of 0xff: left alone
+
+
+def internal_shortest_separator(start: bytes, limit: bytes) -> bytes:
+    """InternalKeyComparator.findShortestSeparator (:77-92): on the user keys."""
+    us, ul = start[:-8], limit[:-8]
+    t = bytewise_shortest_separator(us, ul)
+    if len(t) < len(us) and us < t:
+        return t + SEEK_TAG
+    return start
+
+
+def internal_short_successor(key: bytes) -> bytes:
+    """InternalKeyComparator.findShortSuccessor (:97-109)."""
+    uk = key[:-8]
+    t = bytewise_short_successor(uk)
+    if len(t) < len(uk) and uk < t:
+        return t + SEEK_TAG
+    return key
+
+
+COMPARATORS = {
+    "bytewise": (bytewise_shortest_separator, bytewise_short_successor),
+    "internal": (internal_shortest_separator, internal_short_successor),
+}
 
 
 class BlockBuilder:
@@ -88,10 +145,13 @@ class BlockBuilder:
 
 
 def build_table(pairs, block_size: int = 4096, restart_interval: int = 16, filter_block: bytes | None = None,
-                type_byte: int = 0):
+                type_byte: int = 0, comparator: str = "bytewise"):
     """SSTable image from sorted (key, value) pairs.  Returns (bytes, handles)
     with handles = [(offset, size, kind)] of every block the walker must find:
-    data blocks in index order, the filter block, the metaindex, the index."""
+    data blocks in index order, the filter block, the metaindex, the index.
+    `comparator`: "bytewise" (Options' default) or "internal" (the DB's tables:
+    keys are internal keys, user key || 8-byte tag)."""
+    separator, successor = COMPARATORS[comparator]
     out = bytearray()
     handles = []
 
@@ -105,21 +165,25 @@ def build_table(pairs, block_size: int = 4096, restart_interval: int = 16, filte
     data = BlockBuilder(restart_interval)
     index = BlockBuilder(1)  # index blocks restart at every entry (TableBuilder.java:84)
     last_key = b""
+    pending = None  # handle of the last flushed data block, indexed at the next add / finish
     for key, value in pairs:
+        if pending is not None:  # TableBuilder.add :138-145: separator between the blocks
+            index.add(separator(last_key, key), varint(pending[0]) + varint(pending[1]))
+            pending = None
         data.add(key, value)
         last_key = key
         if data.size_estimate() >= block_size:  # TableBuilder.add -> flush
-            off, size = write_raw(data.finish(), KIND_DATA)
-            index.add(last_key, varint(off) + varint(size))
+            pending = write_raw(data.finish(), KIND_DATA)
             data = BlockBuilder(restart_interval)
-    if not data.empty():
-        off, size = write_raw(data.finish(), KIND_DATA)
-        index.add(last_key, varint(off) + varint(size))
+    if not data.empty():  # finish -> flush
+        pending = write_raw(data.finish(), KIND_DATA)
     meta = BlockBuilder(restart_interval)
     if filter_block is not None:
         foff, fsize = write_raw(filter_block, KIND_META)
         meta.add(b"filter.leveldb.BuiltinBloomFilter2", varint(foff) + varint(fsize))
     moff, msize = write_raw(meta.finish(), KIND_METAINDEX)
+    if pending is not None:  # TableBuilder.finish :221-228: the last block under a short successor
+        index.add(successor(last_key), varint(pending[0]) + varint(pending[1]))
     ioff, isize = write_raw(index.finish(), KIND_INDEX)
     footer = varint(moff) + varint(msize) + varint(ioff) + varint(isize)
     footer += b"\0" * (40 - len(footer)) + struct.pack("<II", MAGIC & 0xFFFFFFFF, MAGIC >> 32)

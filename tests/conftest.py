@@ -36,6 +36,11 @@ def gpu(jl):
     assert torch.cuda.is_available(), "GPU test collected on a machine without a GPU"
     torch.cuda.set_device(0)
     jl.init(0)
+    # the parity tests exercise the device path at every size: small host-memory
+    # calls would otherwise take the SSE4.2 host path (JL_OPT_HOST_THRESHOLD,
+    # tested on its own in test_gpu_dispatch.py)
+    jl.set_option(jl.OPT_HOST_THRESHOLD, 0)
+    jl.set_option(jl.OPT_LOG_HOST_THRESHOLD, 0)
     return torch.device("cuda:0")
 
 

@@ -22,7 +22,10 @@
 //     random initial offsets and capacities and compared record for record and
 //     report for report with the oracle's LogReader (orc_log_read);
 //   * the oracle's own walks (orc_log_events, orc_table_verify, orc_batch) on
-//     random bytes.
+//     random bytes;
+//   * the small-call host paths (host_paths.cpp, JL_OPT_HOST_THRESHOLD): the
+//     log walk on corrupted / random logs event for event, table verify and
+//     batch (init, suffix, mask) block for block, against the oracle.
 // Usage: fuzz_host <iterations> <sstable.bin> <table.bin>   (prints "OK n" on success)
 #include <cstdint>
 #include <cstdio>
@@ -33,6 +36,7 @@
 #include <vector>
 
 #include "../../include/jlcrc.h"
+#include "host_paths.hpp"
 
 extern "C" {
 typedef struct {
@@ -264,6 +268,95 @@ static void fuzz_oracle() {
     if (b.size() > 5) (void)orc_table_verify(b.data(), 0, b.size() - 5);
 }
 
+// ---- host paths (the small-call dispatch) vs the oracle
+static void fuzz_host_paths() {
+    // a log: LogWriter records (dense or sparse), corrupted, or random bytes
+    std::vector<uint8_t> log;
+    if (rnd(4)) {
+        const uint64_t n = rnd(400);
+        std::vector<uint32_t> len(n);
+        std::vector<uint64_t> src(n);
+        uint64_t total = 0;
+        const uint32_t mx = rnd(2) ? 40 : (rnd(2) ? 2000 : 70000);
+        for (uint64_t r = 0; r < n; r++) {
+            len[r] = (uint32_t)rnd(mx);
+            src[r] = total;
+            total += len[r];
+        }
+        std::vector<uint8_t> payload(total ? total : 1);
+        for (auto &b : payload) b = (uint8_t)rng();
+        std::vector<uint8_t> buf(total + 7 * (2 * n + total / 32761 + 2) + 32768);
+        const uint64_t lb = orc_log_write(payload.data(), src.data(), len.data(), n, 0, buf.data(), buf.size());
+        CHECK(lb != ~0ull);
+        log.assign(buf.begin(), buf.begin() + lb);
+        if (rnd(3)) mutate(log);
+    } else {
+        log.resize(rnd(3 * 32768 + 10));
+        for (auto &x : log) x = rnd(4) ? 0 : (uint8_t)rng();
+    }
+    uint8_t *img = (uint8_t *)malloc(log.size() ? log.size() : 1);
+    if (!log.empty()) memcpy(img, log.data(), log.size());
+    const int checksum = (int)rnd(2);
+    std::vector<orc_event> want(log.size() / 7 + 2);
+    const uint64_t wn = orc_log_events(img, log.size(), checksum, want.data(), want.size());
+    // the engine's event form counts the events a failing crc drops (kind 0, as
+    // the device path does); the oracle stops the block there: compare the live ones
+    uint64_t gn = 0;
+    jlhost::log_verify(img, log.size(), checksum, nullptr, 0, &gn);
+    CHECK(gn >= wn);
+    const uint64_t cap = rnd(4) ? gn : rnd(gn + 1);
+    std::vector<jl_log_event> got(cap ? cap : 1);
+    uint64_t gn2 = 0;
+    jlhost::log_verify(img, log.size(), checksum, got.data(), cap, &gn2);
+    CHECK(gn2 == gn);
+    if (cap == gn) {
+        uint64_t j = 0;
+        for (uint64_t i = 0; i < gn; i++) {
+            if (got[i].kind == 0) continue;
+            CHECK(j < wn);
+            CHECK(got[i].offset == want[j].offset && got[i].length == want[j].length && got[i].type == want[j].type &&
+                  got[i].kind == want[j].kind);
+            j++;
+        }
+        CHECK(j == wn);
+    }
+    // blocks of the log bytes: table verify (with planted trailers) and batch
+    const uint64_t n = 1 + rnd(40);
+    std::vector<uint64_t> off(n);
+    std::vector<uint32_t> len(n), init(n), out(n), ref(n);
+    std::vector<uint8_t> sfx(n), st(n);
+    std::vector<uint8_t> b(log.size() + 6);
+    memcpy(b.data(), img, log.size());
+    for (uint64_t i = 0; i < n; i++) {
+        off[i] = rnd(b.size() - 5);
+        len[i] = (uint32_t)rnd(b.size() - 5 - off[i] + 1);
+        init[i] = (uint32_t)rng();
+        sfx[i] = (uint8_t)rng();
+    }
+    const uint32_t flags = (uint32_t)rnd(2);
+    const bool wi = rnd(2), ws = rnd(2);
+    jlhost::batch(b.data(), off.data(), len.data(), wi ? init.data() : nullptr, ws ? sfx.data() : nullptr, n, flags,
+                  out.data());
+    orc_batch(b.data(), off.data(), len.data(), wi ? init.data() : nullptr, ws ? sfx.data() : nullptr, n, flags,
+              ref.data(), 1);
+    CHECK(out == ref);
+    for (uint64_t i = 0; i < n; i++) {  // table blocks: handle (off, size) with size + 5 inside the buffer
+        if (len[i] > 0 && rnd(2)) {
+            const uint32_t sz = len[i] - 1;
+            const uint32_t m = orc_mask(orc_value(b.data() + off[i], (size_t)sz + 1));
+            if (off[i] + sz + 5 <= b.size()) memcpy(b.data() + off[i] + sz + 1, &m, 4);
+        }
+    }
+    std::vector<uint32_t> tsz(n);
+    for (uint64_t i = 0; i < n; i++) {
+        tsz[i] = len[i] ? len[i] - 1 : 0;
+        if (off[i] + tsz[i] + 5 > b.size()) off[i] = 0, tsz[i] = 0;
+    }
+    jlhost::table_verify(b.data(), off.data(), tsz.data(), n, st.data());
+    for (uint64_t i = 0; i < n; i++) CHECK(st[i] == (orc_table_verify(b.data(), off[i], tsz[i]) ? 1 : 0));
+    free(img);
+}
+
 int main(int argc, char **argv) {
     if (argc < 4) {
         fprintf(stderr, "usage: %s iterations sstable.bin table.bin\n", argv[0]);
@@ -276,6 +369,7 @@ int main(int argc, char **argv) {
         if (i % 4 == 0) fuzz_layout();
         if (i % 4 == 1) fuzz_reader();
         if (i % 4 == 2) fuzz_oracle();
+        if (i % 4 == 3) fuzz_host_paths();
         // the scalar statics on odd lengths / alignments
         std::vector<uint8_t> s(rnd(300));
         for (auto &x : s) x = (uint8_t)rng();

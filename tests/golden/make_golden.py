@@ -186,13 +186,16 @@ def main() -> None:
     # ---- a whole SSTable (oracle/sstable.py restatement of TableBuilder), shaped
     # like TestCorruption.build(100): keys "%016d" + 8-byte internal-key tag,
     # 1000-byte values (TestCorruption.java:68, 125-143, 574-584), 4 KiB blocks,
-    # plus a filter block behind the metaindex.  Handles = the walker's expected output.
+    # plus a filter block behind the metaindex, index keys shortened by the
+    # InternalKeyComparator as the DB's TableBuilder does (TableBuilder.java:138-145,
+    # 221-228).  Handles = the walker's expected output.
     from oracle import sstable
 
     srng = np.random.default_rng(0x53535442)
     pairs = [(b"%016d" % i + struct.pack("<Q", (i + 1) << 8 | 1), srng.integers(0, 256, 1000, dtype=np.uint8).tobytes())
              for i in range(100)]
-    sst, sh = sstable.build_table(pairs, filter_block=srng.integers(0, 256, 300, dtype=np.uint8).tobytes())
+    sst, sh = sstable.build_table(pairs, filter_block=srng.integers(0, 256, 300, dtype=np.uint8).tobytes(),
+                                  comparator="internal")  # a DB table: internal keys, InternalKeyComparator
     assert sstable.walk(sst) == sh
     with open(os.path.join(HERE, "sstable.bin"), "wb") as f:
         f.write(sst)

@@ -1,0 +1,84 @@
+"""The small-call dispatch of the host-memory entry points (JL_OPT_HOST_THRESHOLD,
+jleveldb_amd/csrc/host_paths.cpp): below the threshold a call runs on the
+host's SSE4.2 path, above it on the device; both must give identical outputs —
+events (kind-0 drops included), statuses, crcs — on the shapes the reference
+verifies one at a time: one table of <= 2 MiB (Options.java:208,
+TableCache.java:198-208) and one WAL of <= 4 MiB (Options.java:203,
+DBImpl.java:903), with corruption.  Checked against the oracle too.
+"""
+import numpy as np
+import pytest
+
+from jleveldb_amd import workloads as wl
+
+pytestmark = pytest.mark.gpu
+SEED = 0x4A4C4442
+
+
+def _both(jl, engine_options, fn):
+    for opt in (jl.OPT_HOST_THRESHOLD, jl.OPT_LOG_HOST_THRESHOLD):
+        engine_options(opt, 1 << 40)  # host path
+    h = fn()
+    for opt in (jl.OPT_HOST_THRESHOLD, jl.OPT_LOG_HOST_THRESHOLD):
+        engine_options(opt, 0)  # device path
+    d = fn()
+    return h, d
+
+
+def _live(ev):
+    ev = ev[ev["kind"] != 0]
+    return np.stack([ev["offset"], ev["length"].astype(np.uint64), ev["type"].astype(np.uint64),
+                     ev["kind"].astype(np.uint64)])
+
+
+@pytest.mark.parametrize("shape", ["wal_4mib_1056", "wal_dense_131", "wal_mixed", "tiny"])
+def test_log_dispatch_identical(gpu, jl, oracle, engine_options, shape):
+    rng = np.random.default_rng(["wal_4mib_1056", "wal_dense_131", "wal_mixed", "tiny"].index(shape))
+    if shape == "tiny":
+        sizes = rng.integers(0, 300, 5).tolist()
+    elif shape == "wal_mixed":
+        sizes = rng.integers(0, 70000, 60).tolist()
+    else:
+        n = wl.C1_PAYLOAD if shape == "wal_4mib_1056" else wl.DBBENCH_PAYLOAD
+        sizes = [n] * ((4 << 20) // (n + 7))
+    log = bytearray(oracle.log_write([rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]))
+    for _ in range(3):
+        log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
+    log = bytes(log)
+    for checksum in (0, 1):
+        h, d = _both(jl, engine_options, lambda: jl.log_verify(log, checksum))
+        assert h.size == d.size and np.array_equal(h, d)  # the same events, drops included
+        assert np.array_equal(_live(h), _live(oracle.log_events(log, bool(checksum))))
+    recs_h, recs_d = _both(jl, engine_options, lambda: jl.log_read_records(log))
+    assert recs_h == recs_d == oracle.log_read(log)
+
+
+def test_table_batch_fixed_dispatch_identical(gpu, jl, oracle, engine_options):
+    rng = np.random.default_rng(SEED)
+    sizes = rng.integers(3900, 4400, 480).astype(np.uint32)  # one 2 MiB table of ~4.2 KB blocks
+    offs = wl.packed_offsets(sizes + 5)
+    data = rng.integers(0, 256, int(offs[-1]) + int(sizes[-1]) + 5 + 48, dtype=np.uint8)
+    crc = oracle.batch(data, offs, sizes + 1, flags=1)
+    for i in range(sizes.size):
+        p = int(offs[i]) + int(sizes[i]) + 1
+        data[p:p + 4] = np.frombuffer(int(crc[i]).to_bytes(4, "little"), np.uint8)
+    data[int(offs[7]) + 100] ^= 1
+    h, d = _both(jl, engine_options, lambda: jl.table_verify(data, offs, sizes))
+    assert np.array_equal(h, d) and np.nonzero(h == 0)[0].tolist() == [7]
+    init = rng.integers(0, 1 << 32, sizes.size, dtype=np.uint64).astype(np.uint32)
+    sfx = rng.integers(0, 256, sizes.size).astype(np.uint8)
+    for kw in ({}, {"init": init, "suffix": sfx}):
+        for flags in (0, 1):
+            h, d = _both(jl, engine_options, lambda: jl.crc32c_batch(data, offs, sizes, flags=flags, **kw))
+            assert np.array_equal(h, d)
+            assert np.array_equal(h, oracle.batch(data, offs, sizes, flags=flags, **kw))
+    h, d = _both(jl, engine_options, lambda: jl.crc32c_fixed(data[: 300 * 4096], 4096))
+    assert np.array_equal(h, d) and np.array_equal(h, oracle.fixed(data[: 300 * 4096], 4096, 300))
+
+
+def test_threshold_option(jl, gpu, engine_options):
+    for opt in (jl.OPT_HOST_THRESHOLD, jl.OPT_LOG_HOST_THRESHOLD):
+        engine_options(opt, 12345)
+        assert jl.get_option(opt) == 12345
+        with pytest.raises(jl.JLError):
+            jl.set_option(opt, -1)

@@ -12,12 +12,13 @@
   exactly one CRC.
 * C5: 2^17 x 32 KiB log blocks (4 GiB) written by the product's batched
   LogWriter (jl_log_layout + jl_log_emit_dev, J/db/LogWriter.java:88-161) from
-  both payload sets (1 056-B C1-shaped records; mixed 1 B - 100 KiB records that
-  fragment FIRST/MIDDLE/LAST), verified device-resident (jl_log_verify_dev) and
-  compared event-for-event with the oracle's readPhysicalRecord walk
-  (J/db/LogReader.java:297-383), clean and with byte flips in three blocks;
-  plus a 256 MiB log of 0-40 B records (every block past the walk's 64 event
-  slots: the exact-mode re-walk at scale).
+  the three payload sets bench.py reports (1 056-B C1-shaped records; mixed
+  1 B - 100 KiB records that fragment FIRST/MIDDLE/LAST; DBBench-default 131-B
+  records, every block dense), verified device-resident (jl_log_verify_dev and
+  the asynchronous form) and compared event-for-event with the oracle's
+  readPhysicalRecord walk (J/db/LogReader.java:297-383), clean and with byte
+  flips in three blocks; plus a 256 MiB log of 0-40 B records of random lengths
+  (~1 200 events per block: dense blocks whose walk cannot speculate).
 """
 import numpy as np
 import pytest
@@ -59,19 +60,18 @@ def test_full_size_c3_block_for_block(gpu, jl, oracle):
     assert list(np.nonzero(got2 != got)[0]) == [victim]
 
 
-@pytest.mark.parametrize("payloads", ["c1_1056", "mixed_1b_100k", "short_0_40"])
+@pytest.mark.parametrize("payloads", list(wl.C5_SETS) + ["short_0_40"])
 def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
     import torch
 
     if payloads == "short_0_40":
-        # 0-40 B records, 256 MiB of log: ~1 200 events per 32 KiB block, so
-        # every block overflows the walk's 64 slots (the exact mode re-walks
-        # past them in lc_build), flips included
+        # 0-40 B records, 256 MiB of log: ~1 200 events per 32 KiB block, every
+        # block dense (lc_dense), flips included
         rng = np.random.default_rng(SEED + 11)
         lens = rng.integers(0, 41, (256 << 20) // 27).astype(np.uint32)
         lens = lens[: int(np.searchsorted(np.cumsum(lens.astype(np.uint64) + 7), 256 << 20))]
     else:
-        lens = wl.c5_lengths(payloads == "mixed_1b_100k", seed=SEED)  # the sets bench.py reports
+        lens = wl.c5_lengths(payloads, seed=SEED)  # the sets bench.py reports
     offs = wl.packed_offsets(lens)
     plan = jl.log_layout(offs, lens)
     src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
@@ -87,6 +87,12 @@ def test_full_size_c5_log_verify(gpu, jl, oracle, payloads):
         want = oracle.log_events(log.cpu().numpy())
         g, w = _live(got), _live(want)
         assert g.shape == w.shape and np.array_equal(g, w)
+        # the asynchronous form: complete events for any density, no second call
+        ev2 = torch.zeros(n * 16, dtype=torch.uint8, device=gpu)
+        _, res = jl.log_verify_dev_async(log, events=ev2)
+        r = res.cpu().numpy()
+        assert int(r[0]) == n and int(r[2]) == 0
+        assert torch.equal(ev2, ev[: n * 16])
         return want
 
     w = check()

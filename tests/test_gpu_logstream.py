@@ -143,3 +143,36 @@ def test_device_resident_matches(gpu, jl, oracle):
         ev, n = jl.log_verify_dev(d, mode)
         got = ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)
         assert _live(got) == _live(oracle.log_events(bytes(log)))
+
+
+@pytest.mark.parametrize("case", ["equal_131", "equal_0", "equal_400", "random_0_200", "runs", "stops"])
+def test_dense_blocks(gpu, jl, oracle, case):
+    """Blocks of more than 64 records (lc_dense: the block staged in LDS, its
+    headers walked with 64-lane speculation, one thread per record's crc): runs
+    of equal records (the speculation's case: 64 headers per round), random
+    lengths (one header per round), runs that change length mid-block, and
+    every stop decision inside a dense block (bad length, zero-type skip, a
+    failing crc, EOF cases of a short last block), flips included."""
+    rng = np.random.default_rng(["equal_131", "equal_0", "equal_400", "random_0_200", "runs", "stops"].index(case))
+    if case.startswith("equal"):
+        sizes = [int(case.split("_")[1])] * (3 * 32768 // (int(case.split("_")[1]) + 7) + 50)
+    elif case == "random_0_200":
+        sizes = rng.integers(0, 201, 1500).tolist()
+    elif case == "runs":
+        sizes = sum(([int(n)] * int(k) for n, k in zip(rng.integers(0, 300, 40), rng.integers(1, 90, 40))), [])
+    else:
+        sizes = [120] * 1200
+    log = bytearray(oracle.log_write(_payloads(rng, sizes)))
+    if case == "stops":
+        blk = lambda b, o: b * 32768 + o  # noqa: E731
+        log[blk(0, 127 * 10 + 4):blk(0, 127 * 10 + 6)] = b"\xff\x7f"  # bad length in block 0
+        log[blk(1, 5000)] ^= 0x20  # a payload flip: BAD_CRC, rest of block 1 dropped
+        h = 32768 * 2 + 127 * 100  # a header of block 2 (127-B records: the layout does not depend on the seed)
+        log[h + 4:h + 7] = b"\0\0\0"  # zero type, zero length: the rest of block 2 skipped
+        log = log[: len(log) - 3]  # EOF inside the last record
+    else:
+        for _ in range(4):
+            log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
+    log = bytes(log)
+    want = _check(jl, oracle, log, read_records=True)
+    assert len(want) > 65

@@ -312,10 +312,10 @@ def test_log_dev_resident(gpu, jl, oracle):
 
 def test_log_dev_async(gpu, jl, oracle):
     """jl_log_verify_dev_async: several logs verified back to back on one stream
-    with no host round trip (a corrupted one, a tiny one, an empty one), then
-    checked against the oracle from their device result words; a log with more
-    than 64 records in a block reports it in result[1] (verify it with the
-    synchronous call)."""
+    with no host round trip (a corrupted one, a tiny one, an empty one, and one of
+    0-30 B records whose blocks are all dense), then checked against the oracle
+    from their device result words: complete events for every density, the
+    dense blocks counted in result[1]."""
     import torch
 
     rng = np.random.default_rng(41)
@@ -327,20 +327,21 @@ def test_log_dev_async(gpu, jl, oracle):
             log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
         logs.append(bytes(log))
     logs.append(b"")
+    dense = bytearray(oracle.log_write([rng.integers(0, 256, int(s), dtype=np.uint8).tobytes()
+                                        for s in rng.integers(0, 30, 6000)]))
+    dense[40_000] ^= 0x02  # a flip inside a dense block
+    logs.append(bytes(dense))
     runs = []
     for log in logs:
         d = to_dev(np.frombuffer(log, np.uint8), gpu) if log else torch.empty(0, dtype=torch.uint8, device=gpu)
         ev = torch.empty((len(log) // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
         runs.append((log, d, *jl.log_verify_dev_async(d, True, events=ev)))
     for log, d, ev, res in runs:
-        n, over, capf = (int(x) for x in res.cpu().numpy())
-        assert over == 0 and capf == 0
+        n, n_dense, capf = (int(x) for x in res.cpu().numpy())
+        assert capf == 0
+        assert (n_dense > 0) == (log is logs[-1])
         got = np.frombuffer(ev.cpu().numpy().tobytes()[: n * 16], dtype=jl.LOG_EVENT_DTYPE)
         assert _events(got) == _events(oracle.log_events(log))
-    payloads = [bytes(int(s)) for s in rng.integers(0, 30, 3000)]
-    d = to_dev(np.frombuffer(oracle.log_write(payloads), np.uint8), gpu)
-    _, res = jl.log_verify_dev_async(d, True, events=torch.empty(16 * 8000, dtype=torch.uint8, device=gpu))
-    assert int(res[1]) > 0  # blocks past the walk's slots: the caller re-verifies synchronously
 
 
 # ----------------------------------------------------------------- helpers

@@ -164,3 +164,49 @@ def test_concurrent_callers(jl, oracle, arena, log_image):
     for x in th:
         x.join()
     assert not errs, errs
+
+
+def test_async_then_host_call_share_scratch(gpu, jl, oracle, log_image):
+    """A verification left in flight by jl_log_verify_dev_async on torch's default
+    (null) stream, then at once a host jl_log_verify of another log (the
+    workspace's own stream) and a synchronous device call on a side stream: the
+    later calls reuse the thread's scratch only after the async call is done
+    (a completion event, not the stream handle, tracks it: NULL is a valid
+    stream).  All three results equal the oracle's."""
+    import torch
+
+    a = torch.from_numpy(log_image[: 96 << 20].copy()).to(gpu)
+    ev = torch.zeros((a.numel() // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
+    assert torch.cuda.current_stream().cuda_stream == 0  # the null stream
+    _, res = jl.log_verify_dev_async(a, events=ev)
+    host = log_image[CH:]
+    got_h = jl.log_verify(host)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        ev2, n2 = jl.log_verify_dev(a)
+    side.synchronize()
+    torch.cuda.synchronize()
+    n = int(res.cpu()[0])
+    want_a = _live(oracle.log_events(log_image[: 96 << 20]))
+    assert np.array_equal(_live(ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)), want_a)
+    assert np.array_equal(_live(ev2[: n2 * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)), want_a)
+    assert np.array_equal(_live(got_h), _live(oracle.log_events(host)))
+
+
+@pytest.mark.parametrize("mode", ["staged", "pinned"])
+def test_dense_log_host(gpu, jl, oracle, engine_options, mode):
+    """~150 MiB DBBench-default log (131-B payloads: every 32 KiB block dense) with
+    flips, through the host pipeline: the dense blocks' events equal the oracle's."""
+    import torch
+
+    lens = wl.c5_lengths("dbbench_131", target=150 << 20, seed=SEED)
+    plan = jl.log_layout(wl.packed_offsets(lens), lens)
+    src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(src, SEED + 13)
+    log = jl.log_emit_dev(src, plan).cpu().numpy().copy()
+    for at in (CH - 32768 + 17, CH + 5, 2 * CH + 300_001):
+        log[at] ^= 0x04
+    buf = _as_mode(jl, engine_options, log, mode)
+    g, w = _live(jl.log_verify(buf)), _live(oracle.log_events(log))
+    assert g.shape == w.shape and np.array_equal(g, w)
+    assert int((w[3] == jl.LOG_BAD_CRC).sum()) + int((w[3] == jl.LOG_BAD_LENGTH).sum()) >= 3

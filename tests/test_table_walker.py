@@ -112,11 +112,12 @@ def test_error_messages(jl):
     cases["bad block contents"] = _patch_crc(bytes(t), ioff, isize)
     small, sh = _table(1, filt=False)  # one ~1 KiB data block at offset 0: handle bytes 00 xx 08
     so, ss, _ = sh[-1]
+    hs = so + 3 + small[so + 1] + 1  # the index entry's handle: after 3 varints, the key, offset varint 0
     t = bytearray(small)  # its size becomes 16383: past the end of the file
-    t[so + 3 + 25:so + 3 + 27] = b"\xff\x7f"
+    t[hs:hs + 2] = b"\xff\x7f"
     cases["truncated block read"] = _patch_crc(bytes(t), so, ss)
     t = bytearray(small)  # the handle's size varint never terminates inside the value
-    t[so + 3 + 25:so + 3 + 27] = b"\xff\xff"
+    t[hs:hs + 2] = b"\xff\xff"
     cases["bad block handle"] = _patch_crc(bytes(t), so, ss)
     t = bytearray(buf)  # first entry's key length runs past the restart array
     t[ioff + 1] = 0x7F
@@ -202,3 +203,41 @@ def test_whole_table_random_corruption(gpu, jl, oracle):
     assert [(int(o), int(s), int(k)) for o, s, k in zip(off, size, kind)] == handles
     assert [bool(x) for x in st] == [oracle.table_verify(b, int(o), int(n)) for o, n in zip(off, size)]
     assert 0 < int((st == 0).sum()) < len(handles)
+
+
+def test_index_key_shortening(jl):
+    """The restated comparators (BytewiseComparatorImpl.java:60-94,
+    InternalKeyComparator.java:77-109): the index keys TableBuilder writes
+    (TableBuilder.java:138-145, 221-228) are what the restatement writes."""
+    sep, suc = sstable.bytewise_shortest_separator, sstable.bytewise_short_successor
+    assert sep(b"abcdefg", b"abzzz") == b"abd"
+    assert sep(b"abc", b"abcd") == b"abc"  # a prefix: not shortened
+    assert sep(b"ab\xff", b"ac") == b"ab\xff" and sep(b"a4", b"a5") == b"a4"  # no room between
+    assert suc(b"\xff\xffabc") == b"\xff\xffb" and suc(b"\xff\xff") == b"\xff\xff"
+    tag = struct.pack("<Q", 5 << 8 | 1)
+    assert sstable.internal_shortest_separator(b"abcdefg" + tag, b"abzzz" + tag) == b"abd" + sstable.SEEK_TAG
+    assert sstable.internal_short_successor(b"abc" + tag) == b"b" + sstable.SEEK_TAG
+    assert sstable.SEEK_TAG == bytes.fromhex("01ffffffffffff7f")  # (Long.MAX_VALUE >> 8) << 8 | Value
+    # a table whose keys leave room between blocks: shortened index keys, same handles
+    pairs = [(b"key%05d-%s" % (i, b"x" * (i % 7)), bytes(300)) for i in range(0, 4000, 7)]
+    for cmp in ("bytewise", "internal"):
+        kv = pairs if cmp == "bytewise" else [(k + struct.pack("<Q", (i + 1) << 8 | 1), v)
+                                              for i, (k, v) in enumerate(pairs)]
+        buf, handles = sstable.build_table(kv, comparator=cmp)
+        assert sstable.walk(buf) == handles
+        assert _walk(jl, buf) == handles
+        # the index keys are the separators, not the blocks' last keys
+        ioff, isize, _ = [h for h in handles if h[2] == sstable.KIND_INDEX][0]
+        nres = struct.unpack_from("<I", buf, ioff + isize - 4)[0]
+        lim, pos, key, ikeys = ioff + isize - 4 * (1 + nres), ioff, b"", []
+        while pos < lim:
+            sh, pos = sstable.get_varint(buf, pos, lim)
+            ns, pos = sstable.get_varint(buf, pos, lim)
+            vl, pos = sstable.get_varint(buf, pos, lim)
+            key = key[:sh] + buf[pos:pos + ns]
+            ikeys.append(key)
+            pos += ns + vl
+        data_keys = {k for k, _ in kv}
+        assert len(ikeys) == sum(h[2] == sstable.KIND_DATA for h in handles)
+        assert sum(k not in data_keys for k in ikeys) >= 5  # shortened separators (not data keys)
+        assert ikeys == sorted(ikeys)

@@ -224,14 +224,22 @@ def check(body, max_states=64):
 
 
 if __name__ == "__main__":
+    # asm_ring_check.py FILE.s [SUBSTR]                  full dataflow check of the matching kernels
+    # asm_ring_check.py FILE.s --pinned SUBSTR FIRST LAST  pinned-ring check (the build runs this on
+    #                                                      the product gv4 / log-stream objects)
     text = open(sys.argv[1]).read()
-    sub = sys.argv[2] if len(sys.argv) > 2 else ""
-    bad = 0
+    pinned = len(sys.argv) > 2 and sys.argv[2] == "--pinned"
+    sub = sys.argv[3] if pinned else (sys.argv[2] if len(sys.argv) > 2 else "")
+    bad = seen = 0
     for sym, body in kernels(text).items():
         if sub in sym:
-            p = check(body)
+            seen += 1
+            p = check_pinned(body, int(sys.argv[4]), int(sys.argv[5])) + check_local(body) if pinned else check(body)
             bad += len(p)
             for x in p[:8]:
                 print(sym[:60], x[:240])
+    if pinned and not seen:
+        print("no kernel matches", sub)
+        bad = 1
     print("problems", bad)
     sys.exit(1 if bad else 0)
