@@ -201,6 +201,15 @@ int jl_table_block_handles(const uint8_t *file, uint64_t file_bytes, uint64_t *o
 /* Host-memory form (file = mmap'd .ldb bytes); blocking. */
 int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *off, const uint32_t *size, uint64_t n,
                     uint8_t *status);
+/* Several tables at once: the input tables of a compaction, which
+ * VersionSet.makeInputIterator opens with paranoidChecks
+ * (J/db/VersionSet.java:820-823) and Table.open / TableFormat.readBlock verify
+ * one block at a time.  Table t is files[t][0, file_bytes[t]); its handles are
+ * off/size[first[t] .. first[t+1]) (offsets within table t; first[0] = 0,
+ * first[n_tables] = total handles); status[i] as in jl_table_verify.  Tables
+ * are packed into 64 MiB groups, one H2D copy and one launch per group. */
+int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint64_t *file_bytes, const uint64_t *first,
+                     const uint64_t *off, const uint32_t *size, uint8_t *status);
 
 /* ------------------------------------------------- WAL / MANIFEST log shims */
 /* One physical-record decision of LogReader.readPhysicalRecord

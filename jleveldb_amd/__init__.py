@@ -88,6 +88,7 @@ def lib() -> ctypes.CDLL:
         "jl_table_trailers_dev": (i32, [vp, vp, vp, vp, u64, vp, vp]),
         "jl_table_verify_dev": (i32, [vp, u64, vp, vp, u64, vp, vp]),
         "jl_table_verify": (i32, [vp, u64, vp, vp, u64, vp]),
+        "jl_tables_verify": (i32, [u64, vp, vp, vp, vp, vp, vp]),
         "jl_table_block_handles": (i32, [vp, u64, vp, vp, vp, u64, ctypes.POINTER(u64)]),
         "jl_log_verify_dev": (i32, [vp, u64, i32, vp, u64, ctypes.POINTER(u64), vp]),
         "jl_log_verify_dev_async": (i32, [vp, u64, i32, vp, u64, vp, vp]),
@@ -318,6 +319,29 @@ def table_verify(file, off, size) -> np.ndarray:
     _check(lib().jl_table_verify(f_ptr, f_size, off.ctypes.data, size.ctypes.data, off.size, st.ctypes.data),
            "jl_table_verify")
     return st
+
+
+def tables_verify(tables):
+    """Several tables at once (a compaction's inputs, jl_tables_verify): `tables`
+    = [(file bytes, offsets, sizes), ...]; returns one status array per table."""
+    keep, ptrs, nbytes, offs, sizes, first = [], [], [], [], [], [0]
+    for f, o, z in tables:
+        p, n, k = _host_bytes(f)
+        keep.append(k)
+        ptrs.append(p)
+        nbytes.append(n)
+        offs.append(np.ascontiguousarray(o, dtype=np.uint64))
+        sizes.append(np.ascontiguousarray(z, dtype=np.uint32))
+        first.append(first[-1] + offs[-1].size)
+    P = (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+    fb = np.array(nbytes, dtype=np.uint64)
+    fi = np.array(first, dtype=np.uint64)
+    off = np.concatenate(offs) if offs else np.zeros(0, np.uint64)
+    size = np.concatenate(sizes) if sizes else np.zeros(0, np.uint32)
+    st = np.zeros(max(1, off.size), dtype=np.uint8)
+    _check(lib().jl_tables_verify(len(tables), ctypes.cast(P, ctypes.c_void_p), fb.ctypes.data, fi.ctypes.data,
+                                  off.ctypes.data, size.ctypes.data, st.ctypes.data), "jl_tables_verify")
+    return [st[first[i]:first[i + 1]] for i in range(len(tables))]
 
 
 BLOCK_DATA, BLOCK_INDEX, BLOCK_METAINDEX, BLOCK_META = 0, 1, 2, 3

@@ -1096,6 +1096,95 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
         });
 }
 
+// The input tables of a compaction verified together (VersionSet.makeInputIterator
+// opens every input table with paranoidChecks, J/db/VersionSet.java:820-823): the
+// tables are packed into 64 MiB groups, each group staged into one pinned buffer,
+// copied with one H2D transfer and verified with one launch over all its handles
+// (offsets moved by each table's place in the group), double-buffered like the
+// single-table path.  Small batches take the host path (JL_OPT_HOST_THRESHOLD).
+int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint64_t *file_bytes, const uint64_t *first,
+                     const uint64_t *off, const uint32_t *size, uint8_t *status) {
+    if (int r = ensure_ready()) return r;
+    if (n_tables == 0) return JL_OK;
+    if (!files || !file_bytes || !first) return fail(JL_ERR_INVALID, "jl_tables_verify: null pointer");
+    const uint64_t n = first[n_tables];
+    if (first[0] != 0) return fail(JL_ERR_INVALID, "jl_tables_verify: first[0] must be 0");
+    if (n && (!off || !size || !status)) return fail(JL_ERR_INVALID, "jl_tables_verify: null pointer");
+    uint64_t touched = 0;
+    for (uint64_t t = 0; t < n_tables; t++) {
+        if (first[t + 1] < first[t]) return fail(JL_ERR_INVALID, "jl_tables_verify: handle ranges not ascending");
+        if (first[t + 1] > first[t] && !files[t]) return fail(JL_ERR_INVALID, "jl_tables_verify: null table");
+        for (uint64_t i = first[t]; i < first[t + 1]; i++) {
+            if (off[i] > file_bytes[t] || (uint64_t)size[i] + 5 > file_bytes[t] - off[i])
+                return fail(JL_ERR_INVALID, "jl_tables_verify: truncated block read");  // TableFormat.java:203-206
+            touched += (uint64_t)size[i] + 5;
+        }
+    }
+    if (n == 0) return JL_OK;
+    if ((int64_t)touched < opt().host_threshold) {
+        for (uint64_t t = 0; t < n_tables; t++)
+            jlhost::table_verify(files[t], off + first[t], size + first[t], first[t + 1] - first[t], status + first[t]);
+        return JL_OK;
+    }
+    // groups of whole tables (a table larger than a chunk is a group of its own)
+    struct Group {
+        uint64_t t0, t1, bytes;
+    };
+    std::vector<Group> groups;
+    std::vector<uint64_t> place(n_tables);  // each table's offset in its group
+    for (uint64_t t = 0; t < n_tables; t++) {
+        const uint64_t sz = align256(file_bytes[t]);
+        if (groups.empty() || (groups.back().bytes + sz > JL_STREAM_CHUNK_BYTES && groups.back().t1 > groups.back().t0))
+            groups.push_back({t, t, 0});
+        place[t] = groups.back().bytes;
+        groups.back().t1 = t + 1;
+        groups.back().bytes += sz;
+    }
+    Workspace *w = nullptr;
+    if (int r = get_ws(&w)) return r;
+    uint64_t max_bytes = 0, max_h = 0;
+    for (const Group &g : groups) {
+        max_bytes = std::max(max_bytes, g.bytes);
+        max_h = std::max(max_h, first[g.t1] - first[g.t0]);
+    }
+    for (Slot &sl : w->slot) {
+        JL_HIP(sl.d_in.ensure(max_bytes + kSlack));
+        JL_HIP(sl.d_out.ensure(max_h));
+        JL_HIP(sl.d_desc.ensure(max_h * 12 + 4 * 256));
+    }
+    std::vector<uint64_t> adj;
+    return pipeline(
+        *w, groups.size(),
+        [&](uint64_t gi, Slot &sl) -> int {
+            const Group &g = groups[gi];
+            JL_HIP(hipStreamWaitEvent(sl.st, sl.used, 0));
+            JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
+            JL_HIP(sl.h_data.ensure(g.bytes));
+            for (uint64_t t = g.t0; t < g.t1; t++)
+                par_memcpy((uint8_t *)sl.h_data.p + place[t], files[t], file_bytes[t]);
+            JL_HIP(hipMemcpyAsync(sl.d_in.p, sl.h_data.p, g.bytes, hipMemcpyHostToDevice, sl.st));
+            const uint64_t h0 = first[g.t0], m = first[g.t1] - h0;
+            adj.resize(m);
+            for (uint64_t t = g.t0; t < g.t1; t++)
+                for (uint64_t i = first[t]; i < first[t + 1]; i++) adj[i - h0] = off[i] + place[t];
+            return slot_put_desc(sl, {{adj.data(), m * 8}, {size + h0, m * 4}});
+        },
+        [&](uint64_t gi, Slot &sl) -> int {
+            const Group &g = groups[gi];
+            const uint64_t h0 = first[g.t0], m = first[g.t1] - h0;
+            if (m == 0) return JL_OK;
+            jlk::KParams P = base_params(sl.d_in.p, m, jlk::MODE_TABLE_VERIFY);
+            P.base_bytes = g.bytes;
+            P.off = (const uint64_t *)sl.part[0];
+            P.len = (const uint32_t *)sl.part[1];
+            P.len_add = 1;  // block || type byte
+            P.out8 = (uint8_t *)sl.d_out.p;
+            if (int r = run_general(P, w->stream)) return r;
+            JL_HIP(hipMemcpyAsync(status + h0, sl.d_out.p, m, hipMemcpyDeviceToHost, w->stream));
+            return JL_OK;
+        });
+}
+
 // --------------------------------------------------------------- log shims
 int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint8_t *d_type,
                        uint64_t n, uint8_t *d_header, void *stream) {
@@ -1258,9 +1347,9 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
-    // dense blocks: verified whole, exact counts, events stashed (2 workgroups per CU)
+    // dense blocks: verified whole, exact counts, events stashed
     JL_HIP(jlk::launch_lc_walk(A, st));
-    JL_HIP(jlk::launch_lc_dense(A, ctx().cus * 2, st));
+    JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
     size_t t1 = 0, t2 = 0;
     JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, it, A.start, (int)(nb + 1), st));

@@ -171,7 +171,7 @@ hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
-hipError_t launch_lc_dense(const LCArgs &A, int grid, hipStream_t st);
+hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
 
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)

@@ -509,6 +509,35 @@ struct LDSched {
 __device__ __forceinline__ bool ld_vec(const LCArgs &A, uint64_t b) {
     return b < A.n_blocks && A.size - b * 32768u >= 32768u && ((uintptr_t)(A.log + b * 32768u) & 15u) == 0;
 }
+// A thread's 8 x 16 B of the next block, in named registers (an array here was
+// placed in scratch memory by the compiler: every prefetched byte written out
+// and read back, r3e PMC WRITE_SIZE 4.4 GB per 4 GiB log)
+typedef uint32_t ld_v4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 is a union-based class)
+struct LDPre {
+    ld_v4 a, b, c, d, e, f, g, h;
+    __device__ __forceinline__ void load(const uint8_t *blk, uint32_t t) {
+        const ld_v4 *s = (const ld_v4 *)blk + t;
+        a = s[0 * kLDThreads];
+        b = s[1 * kLDThreads];
+        c = s[2 * kLDThreads];
+        d = s[3 * kLDThreads];
+        e = s[4 * kLDThreads];
+        f = s[5 * kLDThreads];
+        g = s[6 * kLDThreads];
+        h = s[7 * kLDThreads];
+    }
+    __device__ __forceinline__ void store(uint32_t *dat, uint32_t t) const {
+        ld_v4 *d4 = (ld_v4 *)dat + t;
+        d4[0 * kLDThreads] = a;
+        d4[1 * kLDThreads] = b;
+        d4[2 * kLDThreads] = c;
+        d4[3 * kLDThreads] = d;
+        d4[4 * kLDThreads] = e;
+        d4[5 * kLDThreads] = f;
+        d4[6 * kLDThreads] = g;
+        d4[7 * kLDThreads] = h;
+    }
+};
 
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];          // the block (+ zero pad: header reads near its end)
@@ -530,18 +559,15 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     LDSched sch;
     sch.init(A);
     uint64_t b = sch.next(A);
-    uint4 pre[8];
-    if (ld_vec(A, b))
-#pragma unroll
-        for (uint32_t k = 0; k < 8; k++) pre[k] = ((const uint4 *)(A.log + b * 32768u))[k * kLDThreads + t];
+    LDPre pre;
+    if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     while (b < A.n_blocks) {
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
         __syncthreads();  // the previous block's readers of dat / hl / s_* are done
         if (ld_vec(A, b)) {
-#pragma unroll
-            for (uint32_t k = 0; k < 8; k++) ((uint4 *)dat)[k * kLDThreads + t] = pre[k];
+            pre.store(dat, t);
         } else {  // the file's short last block (or an unaligned log): bytes, nothing past its end
             const uint8_t *src = A.log + bs;
             for (uint32_t o = t; o < 8192u; o += kLDThreads) {
@@ -554,9 +580,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         if (t < 4) dat[8192 + t] = 0;
         __syncthreads();
         const uint64_t bn = sch.next(A);  // its bytes load during this block's work
-        if (ld_vec(A, bn))
-#pragma unroll
-            for (uint32_t k = 0; k < 8; k++) pre[k] = ((const uint4 *)(A.log + bn * 32768u))[k * kLDThreads + t];
+        if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
         unsigned long long off = 0;
         if (t < 64) {  // the walk, wave 0
             uint32_t p = 0, n = 0;
@@ -628,8 +652,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     }
 }
 
-hipError_t launch_lc_dense(const LCArgs &A, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(lc_dense_kernel, dim3(grid), dim3(kLDThreads), 0, st, A);
+// as many workgroups per CU as the LDS holds (kLDRep 4: 2, 1 or 2: 3)
+hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
+    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * 256 * kLDRep * 4 + kLDMaxEv * 2 + 64;
+    const int per_cu = (int)(kImageBytes / lds);
+    hipLaunchKernelGGL(lc_dense_kernel, dim3(cus * per_cu), dim3(kLDThreads), 0, st, A);
     return hipGetLastError();
 }
 

@@ -39,6 +39,13 @@ public final class Crc32CNative {
     public static native int tableVerify(ByteBuffer file, long[] offset, int[] size, byte[] status);
 
     /**
+     * The same for several mmap'd tables at once (a compaction's inputs,
+     * VersionSet.makeInputIterator): table t's handles are offset/size[first[t] ..
+     * first[t + 1]), first.length == files.length + 1.
+     */
+    public static native int tablesVerify(ByteBuffer[] files, long[] first, long[] offset, int[] size, byte[] status);
+
+    /**
      * Block handles of a whole mmap'd table (footer, index, metaindex walk):
      * data blocks in index order, meta blocks, metaindex, index.  Returns the
      * handle count (greater than offset.length: grow the arrays and call again)

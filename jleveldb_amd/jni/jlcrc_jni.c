@@ -118,6 +118,61 @@ JNIEXPORT jint JNICALL JFN(tableVerify)(JNIEnv *env, jclass cls, jobject file, j
     return r;
 }
 
+/* Several tables at once (a compaction's inputs, jl_tables_verify): files[t]
+ * are direct ByteBuffers (mmap'd .ldb), table t's handles are off/size[first[t]
+ * .. first[t+1]) (first has files.length + 1 entries).  status[i] = 1 ok / 0
+ * "block checksum mismatch".  Arrays copied in and out as in tableVerify; each
+ * element's local reference is released as soon as its address is taken. */
+JNIEXPORT jint JNICALL JFN(tablesVerify)(JNIEnv *env, jclass cls, jobjectArray files, jlongArray first,
+                                          jlongArray off, jintArray size, jbyteArray status) {
+    (void)cls;
+    jsize nt = (*env)->GetArrayLength(env, files), n = (*env)->GetArrayLength(env, off);
+    if ((*env)->GetArrayLength(env, first) != nt + 1 || (*env)->GetArrayLength(env, size) != n ||
+        (*env)->GetArrayLength(env, status) != n) {
+        throw_(env, "java/lang/IllegalArgumentException", "tablesVerify arguments");
+        return JL_ERR_INVALID;
+    }
+    const uint8_t **fp = malloc((size_t)nt * sizeof(*fp) + 1);
+    uint64_t *fb = malloc((size_t)nt * 8 + 1), *fi = malloc(((size_t)nt + 1) * 8);
+    uint64_t *o = malloc((size_t)n * 8 + 1);
+    uint32_t *s = malloc((size_t)n * 4 + 1);
+    uint8_t *st = malloc((size_t)n + 1);
+    int r = JL_ERR_NOMEM;
+    if (fp && fb && fi && o && s && st) {
+        r = JL_OK;
+        for (jsize t = 0; t < nt && r == JL_OK; t++) {
+            jobject b = (*env)->GetObjectArrayElement(env, files, t);
+            fp[t] = b ? (*env)->GetDirectBufferAddress(env, b) : NULL;
+            jlong cap = b ? (*env)->GetDirectBufferCapacity(env, b) : -1;
+            if (b) (*env)->DeleteLocalRef(env, b);
+            if (!fp[t] || cap < 0) {
+                throw_(env, "java/lang/IllegalArgumentException", "tablesVerify: not a direct buffer");
+                r = JL_ERR_INVALID;
+            }
+            fb[t] = (uint64_t)cap;
+        }
+        if (r == JL_OK) {
+            (*env)->GetLongArrayRegion(env, first, 0, nt + 1, (jlong *)fi);
+            (*env)->GetLongArrayRegion(env, off, 0, n, (jlong *)o);
+            (*env)->GetIntArrayRegion(env, size, 0, n, (jint *)s);
+            if (fi[nt] != (uint64_t)n) {
+                throw_(env, "java/lang/IllegalArgumentException", "tablesVerify: first[n] != handles");
+                r = JL_ERR_INVALID;
+            } else {
+                r = jl_tables_verify((uint64_t)nt, fp, fb, fi, o, s, st);
+                if (r == JL_OK) (*env)->SetByteArrayRegion(env, status, 0, n, (const jbyte *)st);
+            }
+        }
+    }
+    free(st);
+    free(s);
+    free(o);
+    free(fi);
+    free(fb);
+    free((void *)fp);
+    return r;
+}
+
 /* Block handles of a whole .ldb image (direct ByteBuffer): data blocks in
  * index order, meta blocks, metaindex, index (jl_table_block_handles).  Returns
  * the handle count — larger than the arrays when they are too short (grow and

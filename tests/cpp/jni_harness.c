@@ -39,9 +39,10 @@ jstring JFN(lastError)(JNIEnv *, jclass);
 jint JFN(tableVerify)(JNIEnv *, jclass, jobject, jlongArray, jintArray, jbyteArray);
 jlong JFN(tableBlockHandles)(JNIEnv *, jclass, jobject, jlongArray, jintArray, jbyteArray);
 jlong JFN(logVerify)(JNIEnv *, jclass, jobject, jboolean, jobject);
+jint JFN(tablesVerify)(JNIEnv *, jclass, jobjectArray, jlongArray, jlongArray, jintArray, jbyteArray);
 
 /* ------------------------------------------------------------- fake JVM */
-enum { K_BYTE = 1, K_INT, K_LONG, K_DIRECT, K_HEAPBUF, K_CLASS, K_STRING };
+enum { K_BYTE = 1, K_INT, K_LONG, K_DIRECT, K_HEAPBUF, K_CLASS, K_STRING, K_OBJARRAY };
 struct _jobject {
     int kind;
     jsize len;   /* elements (arrays) */
@@ -54,6 +55,7 @@ static int g_fail, g_checks;
 static char g_exc[256];  /* pending exception class ("" = none) */
 static int g_critical;   /* open critical regions */
 static int g_abort_release;
+static int g_local_refs;  /* element references handed out and not yet deleted */
 
 #define CHECK(cond, ...)                                                        \
     do {                                                                        \
@@ -92,7 +94,8 @@ static jint f_ThrowNew(JNIEnv *env, jclass cls, const char *msg) {
 static jsize f_GetArrayLength(JNIEnv *env, jarray a) {
     (void)env;
     jni_rule("GetArrayLength", 0);
-    CHECK(a && (a->kind == K_BYTE || a->kind == K_INT || a->kind == K_LONG), "GetArrayLength of a non-array");
+    CHECK(a && (a->kind == K_BYTE || a->kind == K_INT || a->kind == K_LONG || a->kind == K_OBJARRAY),
+          "GetArrayLength of a non-array");
     return a ? a->len : 0;
 }
 static void *f_GetCritical(JNIEnv *env, jarray a, jboolean *is_copy) {
@@ -160,10 +163,23 @@ static void f_SetIntRegion(JNIEnv *env, jintArray a, jsize s, jsize n, const jin
     if (region_ok("SetIntArrayRegion", a, K_INT, s, n)) memcpy((jint *)a->data + s, buf, (size_t)n * 4);
 }
 
+static jobject f_GetObjectArrayElement(JNIEnv *env, jobjectArray a, jsize i) {
+    (void)env;
+    jni_rule("GetObjectArrayElement", 0);
+    CHECK(a && a->kind == K_OBJARRAY && i >= 0 && i < a->len, "GetObjectArrayElement out of bounds");
+    g_local_refs++;
+    return ((jobject *)a->data)[i];
+}
+static void f_DeleteLocalRef(JNIEnv *env, jobject o) {
+    (void)env;
+    (void)o;
+    g_local_refs--;
+}
+
 static const struct JNINativeInterface_ g_fns = {
     f_FindClass,      f_ThrowNew,        f_GetArrayLength,          f_GetCritical,   f_ReleaseCritical,
     f_NewStringUTF,   f_GetDirectBufferAddress, f_GetDirectBufferCapacity, f_GetLongRegion, f_GetIntRegion,
-    f_SetByteRegion,  f_SetLongRegion,   f_SetIntRegion,
+    f_SetByteRegion,  f_SetLongRegion,   f_SetIntRegion,            f_GetObjectArrayElement, f_DeleteLocalRef,
 };
 static JNIEnv g_env_v = &g_fns;
 static JNIEnv *const env = &g_env_v;
@@ -360,7 +376,44 @@ static void device_paths(const uint8_t *sst, size_t sst_n, const uint8_t *log, s
                   (n < 2 || ((uint8_t *)st->data)[1] == 1), "flipped block not seen");
         free(want);
     }
-    release(o), release(s), release(st), release(buf);
+    release(o), release(s), release(st);
+    /* tablesVerify: the same table three times (a compaction's inputs), one flip in the second copy */
+    {
+        uint8_t *c2 = malloc(sst_n);
+        memcpy(c2, sst, sst_n);
+        c2[wo[n - 1] + 1] ^= 0x04;  /* a byte of the index block */
+        struct _jobject *b1 = direct((void *)sst, (jlong)sst_n), *b2 = direct(c2, (jlong)sst_n);
+        struct _jobject *fa = array(K_OBJARRAY, 3);
+        fa->data = realloc(fa->data, 3 * sizeof(jobject));
+        ((jobject *)fa->data)[0] = b1, ((jobject *)fa->data)[1] = b2, ((jobject *)fa->data)[2] = b1;
+        struct _jobject *fi = array(K_LONG, 4), *to = array(K_LONG, (jsize)(3 * n)), *tz = array(K_INT, (jsize)(3 * n)),
+                        *tst = array(K_BYTE, (jsize)(3 * n));
+        for (int t = 0; t < 4; t++) ((jlong *)fi->data)[t] = (jlong)(t * n);
+        for (int t = 0; t < 3; t++) {
+            memcpy((jlong *)to->data + t * n, wo, n * 8);
+            memcpy((jint *)tz->data + t * n, ws, n * 4);
+        }
+        jint rr = JFN(tablesVerify)(env, NULL, fa, fi, to, tz, tst);
+        CHECK(g_local_refs == 0, "tablesVerify leaked %d local references", g_local_refs);
+        if (!gpu) {
+            CHECK(rr == JL_ERR_NO_DEVICE && g_exc[0] == 0, "tablesVerify without a GPU: %d", rr);
+        } else {
+            CHECK(rr == JL_OK, "tablesVerify: %d", rr);
+            for (uint64_t i = 0; i < 3 * n; i++)
+                CHECK(((uint8_t *)tst->data)[i] == (i == 2 * n - 1 ? 0 : 1), "tablesVerify status %llu", (unsigned long long)i);
+        }
+        ((jlong *)fi->data)[3] = (jlong)(3 * n - 1);  /* first[n] must equal the handle count */
+        CHECK(JFN(tablesVerify)(env, NULL, fa, fi, to, tz, tst) == JL_ERR_INVALID &&
+                  took("java/lang/IllegalArgumentException") && g_local_refs == 0, "tablesVerify bad first");
+        struct _jobject heap = {K_HEAPBUF, 0, c2, (jlong)sst_n, ""};
+        ((jobject *)fa->data)[1] = &heap;
+        ((jlong *)fi->data)[3] = (jlong)(3 * n);
+        CHECK(JFN(tablesVerify)(env, NULL, fa, fi, to, tz, tst) == JL_ERR_INVALID &&
+                  took("java/lang/IllegalArgumentException") && g_local_refs == 0, "tablesVerify heap buffer");
+        release(fi), release(to), release(tz), release(tst), release(fa), release(b1), release(b2);
+        free(c2);
+    }
+    release(buf);
     free(copy);
     free(wo);
     free(ws);

@@ -21,6 +21,7 @@ typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jintArray;
 typedef jarray jlongArray;
+typedef jarray jobjectArray;
 
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
@@ -45,5 +46,7 @@ struct JNINativeInterface_ {
     void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf);
     void (*SetLongArrayRegion)(JNIEnv *env, jlongArray array, jsize start, jsize len, const jlong *buf);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len, const jint *buf);
+    jobject (*GetObjectArrayElement)(JNIEnv *env, jobjectArray array, jsize index);
+    void (*DeleteLocalRef)(JNIEnv *env, jobject obj);
 };
 #endif

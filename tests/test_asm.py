@@ -17,7 +17,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "jleveldb_amd", "csrc")
 UNITS = ([("jlcrc_kernels.hip", []), ("fixed_v4.hip", [])] + [("stream_kernel.hip", [f"-DJL_MODE={m}"]) for m in range(5)]
-         + [("general_v4.hip", [f"-DJL_MODE={m}"]) for m in (0, 1, 2, 5)] + [("log_stream.hip", [])])
+         + [("general_v4.hip", [f"-DJL_MODE={m}"]) for m in (0, 1, 2, 5)] + [("log_stream.hip", []),
+                                                                              ("log_chunks.hip", [])])
 
 
 @pytest.fixture(scope="module")
@@ -101,3 +102,15 @@ def test_no_smem_address_clobbered_inside_an_asm_block(asm):
             bad.append(ins)
         block.append(dst)
     assert not bad, bad[:5]
+
+
+def test_no_scratch_memory(asm):
+    """No kernel keeps anything in scratch (private) memory: r3's lc_dense had its
+    prefetched block bytes (an array of HIP uint4) placed there by the compiler,
+    so every byte was written to memory and read back (PMC WRITE_SIZE 4.4 GB per
+    4 GiB log)."""
+    import re
+
+    sizes = re.findall(r"\.name:\s+(\S+)\n(?:.*\n)*?\s+\.private_segment_fixed_size:\s+(\d+)", asm)
+    assert len(sizes) >= 30
+    assert not [(n, int(z)) for n, z in sizes if int(z)], [(n, int(z)) for n, z in sizes if int(z)][:5]

@@ -82,3 +82,36 @@ def test_threshold_option(jl, gpu, engine_options):
         assert jl.get_option(opt) == 12345
         with pytest.raises(jl.JLError):
             jl.set_option(opt, -1)
+
+
+def _table_file(oracle, rng, mib):
+    """A table-shaped file: ~4.2 KB blocks with valid 5-byte trailers."""
+    sizes = rng.integers(3900, 4400, max(1, int(mib * (1 << 20)) // 4150)).astype(np.uint32)
+    offs = wl.packed_offsets(sizes + 5)
+    data = rng.integers(0, 256, int(offs[-1]) + int(sizes[-1]) + 5 + 48, dtype=np.uint8)
+    crc = oracle.batch(data, offs, sizes + 1, flags=1)
+    for i in range(sizes.size):
+        p = int(offs[i]) + int(sizes[i]) + 1
+        data[p:p + 4] = np.frombuffer(int(crc[i]).to_bytes(4, "little"), np.uint8)
+    return data, offs, sizes
+
+
+@pytest.mark.parametrize("n_tables,mib", [(12, 2.0), (40, 2.0), (3, 70.0)])
+def test_tables_verify_compaction_inputs(gpu, jl, oracle, engine_options, n_tables, mib):
+    """jl_tables_verify over a compaction's input tables (VersionSet.java:820-823):
+    equal to one jl_table_verify per table, flips seen in their own table only;
+    40 x 2 MiB spans two 64 MiB groups, 3 x 70 MiB one group per table."""
+    rng = np.random.default_rng(n_tables)
+    tables = [_table_file(oracle, rng, mib) for _ in range(n_tables)]
+    flipped = sorted({0, n_tables // 2, n_tables - 1})
+    for t in flipped:
+        data, offs, sizes = tables[t]
+        data[int(offs[t % sizes.size]) + 3] ^= 0x20
+    for thr in (0, 1 << 40):  # device, host
+        engine_options(jl.OPT_HOST_THRESHOLD, thr)
+        got = jl.tables_verify(tables)
+        for (data, offs, sizes), st in zip(tables, got):
+            assert np.array_equal(st, jl.table_verify(data, offs, sizes))
+        bad = [(t, int(i)) for t, st in enumerate(got) for i in np.nonzero(st == 0)[0]]
+        want = [(t, t % tables[t][2].size) for t in flipped]
+        assert bad == want
