@@ -475,7 +475,7 @@ __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // 
 }
 
 #ifndef JL_LD_REP
-#define JL_LD_REP 4
+#define JL_LD_REP 2  // r3f A/B on the DBBench set: 1.99 ms (2, 3 workgroups per CU) vs 2.21 (4) and 2.16 (8, both 2 per CU)
 #endif
 constexpr uint32_t kLDThreads = 256, kLDRep = JL_LD_REP;
 // A workgroup's dense blocks: the candidates blockIdx.x + j * gridDim.x, 64 of
