@@ -23,12 +23,14 @@
 // Pipeline.  The loads are inline-asm buffer_load_dwordx4 … nt through a
 // buffer resource per round (num_records = the bytes of the round that exist:
 // reads past the last block return zeros, so ragged tails need no predication).
-// A register ring of P = 16 slots keeps 16 KiB in flight per wave: step k
-// consumes slot k % P after s_waitcnt vmcnt(P-2) and immediately refills it with
-// step k + P (of this round or the next), so the HBM stream never drains,
-// including across the epilogue and group boundaries.  vmcnt is conservative
-// by one so that the one result store per group (vmcnt counts stores on gfx9)
-// can never be mistaken for a completed load.
+// A register ring of P slots keeps P KiB in flight per wave: step k consumes
+// slot k % P after s_waitcnt vmcnt(P-2) and immediately refills it with step
+// k + P (of this round or the next), so the HBM stream never drains, including
+// across the epilogue and group boundaries.  The product instantiation is P = 8
+// slots at 1024 threads (16 waves per CU: 128 KiB in flight per CU; shape 3
+// below); the 16-slot ring at 512 threads survives as a study shape.  vmcnt is
+// conservative by one so that the one result store per group (vmcnt counts
+// stores on gfx9) can never be mistaken for a completed load.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
