@@ -1318,8 +1318,15 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_end = o_res + 256;
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
-    // the dense blocks' events: at most the caller's capacity (more events fail the call anyway)
-    const uint64_t stash_cap = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
+    // the dense blocks' events: at most the caller's capacity (more events fail the call anyway).
+    // With pools (>= 8 blocks per lc_dense workgroup) a workgroup leaves less than a pool
+    // unused at the end, and less than its next block's events (<= kLDMaxEv) per refill:
+    // refills <= events / (pool - kLDMaxEv) + grid
+    const uint64_t need = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
+    const uint64_t grid = jlk::lc_dense_grid(ctx().cus);
+    const uint64_t pool = nb >= 8 * grid ? jlk::kLDPool : 0;
+    const uint64_t stash_cap =
+        pool ? need + (need / (pool - jlk::kLDMaxEv) + grid) * jlk::kLDMaxEv + grid * pool : need;
     JL_HIP(c.ws_stash.ensure(std::max<uint64_t>(stash_cap, 1) * 8));
     char *ws = (char *)c.ws_lc.p;
     jlk::LCArgs A;
@@ -1341,6 +1348,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
+    A.stash_pool = pool;
     if (!c.h_res) JL_HIP(hipHostMalloc((void **)&c.h_res, 64, hipHostMallocCoherent));
     A.result = d_result ? d_result : c.h_res;
     A.ev = (jlk::LogEvent *)d_events;

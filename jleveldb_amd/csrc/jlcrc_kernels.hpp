@@ -148,6 +148,10 @@ struct LCArgs {
     uint64_t *dense_off;
     uint64_t *stash;
     uint64_t stash_cap;
+    // > 0: a workgroup takes stash entries stash_pool at a time (>= kLDMaxEv; one
+    // atomic per many blocks, whose wait would also wait for the prefetch loads);
+    // 0: one atomic per block (small logs)
+    uint64_t stash_pool;
     unsigned long long *stash_ctr;  // zeroed by lc_walk
     uint64_t *start;       // n_blocks + 1: exclusive scan of count
     uint32_t *hist;        // kLCCounters * n_grp + 1, counter-major (hist[c * n_grp + group])
@@ -172,6 +176,8 @@ hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
+uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
+constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
 
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)

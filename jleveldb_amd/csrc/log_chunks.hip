@@ -454,7 +454,7 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // them into 8-chunk rounds would pay a round epilogue per ~2 windows, so a
 // workgroup takes the whole block instead: it stages the block in LDS, walks
 // its headers there, checks every record's crc with one thread per record
-// (slicing-by-4 from LDS tables) and stashes the block's events in file order
+// (kLDSlice / 4 interleaved slicing chains from LDS tables) and stashes the block's events in file order
 // (8 B each) with its exact event count, before the event scan; lc_build copies
 // them to their places.  Persistent grid over the blocks lc_walk marked; each
 // workgroup loads its next dense block into registers while it works on the
@@ -467,17 +467,74 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // records is walked 64 headers per LDS round trip; unequal lengths advance one
 // header per round.
 //
-// Tables: kLDRep copies of T0..T3 interleaved so that copy r sits in banks
+// Tables: kLDRep copies of T0..T_{kLDSlice-1} interleaved so that copy r sits in banks
 // {r, r + kLDRep, ...} and thread t reads copy t mod kLDRep: the random lookups
 // of 32 lanes conflict only among the 32 / kLDRep lanes sharing a copy.
 __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
     return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
 }
 
+// A/B on the DBBench set (whole verification, tools/ab_lib.sh): r3f, slicing-by-4,
+// before the LDS-only barrier: 1.99 ms (2 copies, 3 workgroups per CU) vs 2.21 (4)
+// and 2.16 (8, both 2 per CU); r3j, LDS-only barrier and stash pools: 1.585 ms
+// (slicing 8, 1 copy, 3 per CU) vs 1.72 (4, 2 copies, 3 per CU), 1.94 (16, 1 copy,
+// 2 per CU) and 2.03 (8, 2 copies, 2 per CU)
 #ifndef JL_LD_REP
-#define JL_LD_REP 2  // r3f A/B on the DBBench set: 1.99 ms (2, 3 workgroups per CU) vs 2.21 (4) and 2.16 (8, both 2 per CU)
+#define JL_LD_REP 1
 #endif
-constexpr uint32_t kLDThreads = 256, kLDRep = JL_LD_REP;
+// Slicing width: a record's dwords go round-robin to kLDSlice / 4 independent
+// chains, each advancing kLDSlice bytes per step through T_{S-1}..T_{S-4}, so the
+// dependent LDS round trips per record drop from one per 4 B to one per S bytes
+#ifndef JL_LD_SLICE
+#define JL_LD_SLICE 8
+#endif
+constexpr uint32_t kLDThreads = 256, kLDRep = JL_LD_REP, kLDSlice = JL_LD_SLICE, kLDChains = kLDSlice / 4;
+static_assert(kLDSlice == 4 || kLDSlice == 8 || kLDSlice == 12 || kLDSlice == 16, "slicing width");
+static_assert(kLDPool >= kLDMaxEv, "a fresh stash pool holds any block");
+// T_k[e] (e followed by k zero bytes), this thread's copy
+__device__ __forceinline__ uint32_t ld_t(const uint32_t *T, uint32_t k, uint32_t e) { return T[(256u * k + e) * kLDRep]; }
+// the dword x (the state xor the next 4 data bytes) followed by n - 4 zero bytes
+__device__ __forceinline__ uint32_t ld_adv(const uint32_t *T, uint32_t x, uint32_t n) {
+    return xor3(ld_t(T, n - 1u, x & 0xffu), ld_t(T, n - 2u, (x >> 8) & 0xffu), ld_t(T, n - 3u, (x >> 16) & 0xffu)) ^
+           ld_t(T, n - 4u, x >> 24);
+}
+// k = 1..3 data bytes v (low bytes) into the state x: one round trip
+__device__ __forceinline__ uint32_t ld_absorb(const uint32_t *T, uint32_t x, uint32_t v, uint32_t k) {
+    const uint32_t y = x ^ v;
+    uint32_t r = (x >> (8u * k)) ^ ld_t(T, k - 1u, y & 0xffu);
+    if (k > 1u) r ^= ld_t(T, k - 2u, (y >> 8) & 0xffu);
+    if (k > 2u) r ^= ld_t(T, 0u, (y >> 16) & 0xffu);
+    return r;
+}
+// crc32c state over bytes [q, e) of the staged block from state x
+__device__ __forceinline__ uint32_t ld_crc(const uint32_t *T, const uint32_t *dat, uint32_t x, uint32_t q, uint32_t e) {
+    uint32_t k = (4u - (q & 3u)) & 3u;  // head: up to the next dword
+    if (k > e - q) k = e - q;
+    if (k) {
+        x = ld_absorb(T, x, (dat[q >> 2] >> (8u * (q & 3u))) & ((1u << (8u * k)) - 1u), k);
+        q += k;
+    }
+    const uint32_t *D = dat + (q >> 2);
+    const uint32_t m = (e - q) >> 2, G = m / kLDChains;
+    if (G) {
+        uint32_t c[kLDChains];
+#pragma unroll
+        for (uint32_t j = 0; j < kLDChains; j++) c[j] = j ? 0u : x;
+        for (uint32_t g = 1; g < G; g++, D += kLDChains) {
+#pragma unroll
+            for (uint32_t j = 0; j < kLDChains; j++) c[j] = ld_adv(T, c[j] ^ D[j], kLDSlice);
+        }
+        // the last step of chain j stops at the group's end: kLDSlice - 4 j bytes
+        x = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kLDChains; j++) x ^= ld_adv(T, c[j] ^ D[j], kLDSlice - 4u * j);
+        D += kLDChains;
+    }
+    for (uint32_t j = G * kLDChains; j < m; j++) x = ld_adv(T, x ^ *D++, 4u);
+    q += 4u * m;
+    if (q < e) x = ld_absorb(T, x, dat[q >> 2] & ((1u << (8u * (e - q))) - 1u), e - q);
+    return x;
+}
 // A workgroup's dense blocks: the candidates blockIdx.x + j * gridDim.x, 64 of
 // them per wave-wide load of count[] (the ballot of the dense ones is kept, so a
 // log of dense blocks costs one load per 64 blocks and a log without any costs
@@ -539,9 +596,29 @@ struct LDPre {
     }
 };
 
+// A barrier over LDS only.  __syncthreads() also waits for every outstanding
+// global access (vmcnt(0): gfx950 counts loads and stores together), which held
+// each block's walk until the next block's prefetch had landed (tools/ld_prof.py:
+// ~6 K of ~16 K clocks per block).
+__device__ __forceinline__ void ld_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+#ifndef JL_LD_PROF
+#define JL_LD_PROF 0  // study builds: per-phase shader clocks of lc_dense (tools/ld_prof.py)
+#endif
+#if JL_LD_PROF
+__device__ unsigned long long g_ld_prof[8];
+#define LD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define LD_T(v)
+#endif
+
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];          // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t tab[4 * 256 * kLDRep];  // T_k[e] copy r at word (256 k + e) kLDRep + r
+    __shared__ uint32_t tab[kLDSlice * 256 * kLDRep];  // T_k[e] copy r at word (256 k + e) kLDRep + r
     __shared__ uint16_t hl[kLDMaxEv];           // header offsets of the block's events
     __shared__ uint32_t s_n, s_bad;
     __shared__ unsigned long long s_off;
@@ -549,23 +626,27 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     {  // T0 from aux (crc_math.hpp build_aux), T_k[e] = T_{k-1}[e] >> 8 ^ T0[T_{k-1}[e] & 0xff]
         uint32_t v = A.aux[t];
         for (uint32_t r = 0; r < kLDRep; r++) tab[t * kLDRep + r] = v;
-        for (uint32_t k = 1; k < 4; k++) {
+        for (uint32_t k = 1; k < kLDSlice; k++) {
             v = (v >> 8) ^ A.aux[v & 0xffu];
             for (uint32_t r = 0; r < kLDRep; r++) tab[(256u * k + t) * kLDRep + r] = v;
         }
     }
     const uint32_t *T = tab + rep;
-    const uint8_t *by = (const uint8_t *)dat;
     LDSched sch;
     sch.init(A);
     uint64_t b = sch.next(A);
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
+    unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
+#if JL_LD_PROF
+    uint64_t acc[5] = {0, 0, 0, 0, 0};
+#endif
     while (b < A.n_blocks) {
+        LD_T(ta);
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
-        __syncthreads();  // the previous block's readers of dat / hl / s_* are done
+        ld_sync();  // the previous block's readers of dat / hl / s_* are done
         if (ld_vec(A, b)) {
             pre.store(dat, t);
         } else {  // the file's short last block (or an unaligned log): bytes, nothing past its end
@@ -578,7 +659,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
         }
         if (t < 4) dat[8192 + t] = 0;
-        __syncthreads();
+        ld_sync();
+        LD_T(tb);
         const uint64_t bn = sch.next(A);  // its bytes load during this block's work
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
         unsigned long long off = 0;
@@ -608,26 +690,27 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             if (lane == 0) {
                 s_n = n;
                 s_bad = kLCNone;
-                off = atomicAdd(A.stash_ctr, (unsigned long long)n);  // used after the crcs: its latency hides
+                if (!A.stash_pool) {
+                    off = atomicAdd(A.stash_ctr, (unsigned long long)n);
+                } else {  // a fresh pool holds any block (kLDPool >= kLDMaxEv)
+                    if (pool_hi - pool_lo < n) {
+                        pool_lo = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
+                        pool_hi = pool_lo + A.stash_pool;
+                    }
+                    off = pool_lo;
+                    pool_lo += n;
+                }
             }
         }
-        __syncthreads();
+        ld_sync();
+        LD_T(tc);
         const uint32_t n = s_n;
         if (A.checksum) {  // one thread per OK record: crc over type || payload (J/db/LogWriter.java:147)
             for (uint32_t r = t; r < n; r += kLDThreads) {
                 const uint32_t h = hl[r];
                 const LCDecision d = lc_decide(blen - h, eof, lds32u(dat, h + 3u));
                 if (d.kind != 1u) continue;
-                const uint32_t e = h + 7u + d.length;
-                uint32_t x = 0xffffffffu, q = h + 6u;
-                for (; q < e && (q & 3u); q++) x = (x >> 8) ^ T[((x ^ by[q]) & 0xffu) * kLDRep];
-                for (; q + 4u <= e; q += 4u) {
-                    x ^= dat[q >> 2];
-                    x = xor3(T[(768u + (x & 0xffu)) * kLDRep], T[(512u + ((x >> 8) & 0xffu)) * kLDRep],
-                             T[(256u + ((x >> 16) & 0xffu)) * kLDRep]) ^
-                        T[(x >> 24) * kLDRep];
-                }
-                for (; q < e; q++) x = (x >> 8) ^ T[((x ^ by[q]) & 0xffu) * kLDRep];
+                const uint32_t x = ld_crc(T, dat, 0xffffffffu, h + 6u, h + 7u + d.length);
                 if (mask_crc(~x) != lds32u(dat, h)) atomicMin(&s_bad, r);
             }
         }
@@ -636,7 +719,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             A.count[b] = n;
             A.dense_off[b] = s_off;
         }
-        __syncthreads();
+        ld_sync();
+        LD_T(td);
         // the events in file order (8 B each); the first failing record is BAD_CRC
         // and the rest of the block is dropped (J/db/LogReader.java:359-367)
         const uint32_t bad = s_bad;
@@ -648,17 +732,40 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 const uint64_t kind = r == bad ? 2u : (bad != kLCNone && r > bad ? 0u : d.kind);
                 A.stash[so + r] = h | ((uint64_t)d.length << 16) | ((uint64_t)d.type << 32) | (kind << 40);
             }
+#if JL_LD_PROF
+        LD_T(te);
+        acc[0] += tb - ta;
+        acc[1] += tc - tb;
+        acc[2] += td - tc;
+        acc[3] += te - td;
+        acc[4] += 1;
+#endif
         b = bn;
     }
+#if JL_LD_PROF
+    if (t == 0)
+        for (int i = 0; i < 5; i++) atomicAdd(&g_ld_prof[i], (unsigned long long)acc[i]);
+#endif
 }
 
-// as many workgroups per CU as the LDS holds (kLDRep 4: 2, 1 or 2: 3)
+// as many workgroups per CU as the LDS holds
+uint32_t lc_dense_grid(int cus) {
+    constexpr uint32_t lds = (8192 + 4) * 4 + kLDSlice * 256 * kLDRep * 4 + kLDMaxEv * 2 + 64;
+    return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
+}
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * 256 * kLDRep * 4 + kLDMaxEv * 2 + 64;
-    const int per_cu = (int)(kImageBytes / lds);
-    hipLaunchKernelGGL(lc_dense_kernel, dim3(cus * per_cu), dim3(kLDThreads), 0, st, A);
+    hipLaunchKernelGGL(lc_dense_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);
     return hipGetLastError();
 }
+
+#if JL_LD_PROF
+// study builds: read (and clear) lc_dense's phase clocks [stage, walk, crc, stash, blocks]
+extern "C" int jl_study_ld_prof(unsigned long long *out) {
+    static const unsigned long long zero[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ld_prof), sizeof(zero)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ld_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
     hipLaunchKernelGGL(lc_walk_kernel, dim3((A.n_grp + 3) / 4), dim3(256), 0, st, A);

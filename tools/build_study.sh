@@ -6,4 +6,4 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-make -s -j8 -C jleveldb_amd/csrc STUDY=1 BUILD=_build_$name OUT=../../tools/libjlcrc_$name.so EXTRA="$*"
+make -s -j8 -C jleveldb_amd/csrc STUDY=${STUDY:-1} BUILD=_build_$name OUT=../../tools/libjlcrc_$name.so EXTRA="$*"
