@@ -460,12 +460,12 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // workgroup loads its next dense block into registers while it works on the
 // current one.
 //
-// The walk (one wave) speculates: after a header of length n, lane k reads the
-// header at p + k (7 + n); the lanes up to the first one that is not an OK
+// The walk (one wave) speculates: on the stride L = 7 + n of the last run, lane
+// k reads the headers at p + (k + 64 j) L, j < kLDCand, in the same LDS trip as
+// the header at p itself; the candidates up to the first one that is not an OK
 // record of the same length are the next headers of the chain (the reference's
-// decisions in its order, J/db/LogReader.java:297-383), so a run of equal
-// records is walked 64 headers per LDS round trip; unequal lengths advance one
-// header per round.
+// decisions in its order, J/db/LogReader.java:297-383).  A run of equal records
+// is walked 256 headers per LDS round trip; a new length costs a second trip.
 //
 // Tables: kLDRep copies of T0..T_{kLDSlice-1} interleaved so that copy r sits in banks
 // {r, r + kLDRep, ...} and thread t reads copy t mod kLDRep: the random lookups
@@ -473,12 +473,24 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
     return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
 }
+// header bytes 3..6 at c when a whole header fits before blen, else 0
+__device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uint32_t c) {
+    return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
+}
+#ifndef JL_LD_CAND
+#define JL_LD_CAND 1  // r3n A/B (DBBench set): 1 1.62 ms, 2 1.64, 4 1.73 (more LDS reads per trip)
+#endif
+constexpr uint32_t kLDCand = JL_LD_CAND;  // walk candidates per lane and LDS trip
 
 // A/B on the DBBench set (whole verification, tools/ab_lib.sh): r3f, slicing-by-4,
 // before the LDS-only barrier: 1.99 ms (2 copies, 3 workgroups per CU) vs 2.21 (4)
 // and 2.16 (8, both 2 per CU); r3j, LDS-only barrier and stash pools: 1.585 ms
 // (slicing 8, 1 copy, 3 per CU) vs 1.72 (4, 2 copies, 3 per CU), 1.94 (16, 1 copy,
-// 2 per CU) and 2.03 (8, 2 copies, 2 per CU)
+// 2 per CU) and 2.03 (8, 2 copies, 2 per CU); r3o, two threads per record (front
+// and back 64 B, folded with z^64; 512 threads): 1.70 / 2.24 ms vs 1.61.  PMC
+// r3n: LDS busy ~68 % of the kernel, 58 % of that bank conflicts of the random
+// lookups (one copy), VALU ~30 %: the lookups' LDS cycles bound it, not the
+// length of a record's dependence chain
 #ifndef JL_LD_REP
 #define JL_LD_REP 1
 #endif
@@ -639,7 +651,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
 #if JL_LD_PROF
-    uint64_t acc[5] = {0, 0, 0, 0, 0};
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
     while (b < A.n_blocks) {
         LD_T(ta);
@@ -663,27 +675,46 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         LD_T(tb);
         const uint64_t bn = sch.next(A);  // its bytes load during this block's work
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
+        LD_T(tb2);
         unsigned long long off = 0;
         if (t < 64) {  // the walk, wave 0
-            uint32_t p = 0, n = 0;
+            uint32_t p = 0, n = 0, L = 0;  // L: the last run's stride (7 + length), 0 before the first
             for (;;) {
-                const uint32_t rem = blen - p;
-                const LCDecision d0 = lc_decide(rem, eof, rem >= 7 ? lds32u(dat, p + 3u) : 0u);
+                // one LDS trip: the header at p (lane 0's first candidate) and, on the
+                // last run's stride, the kLDCand * 64 - 1 after it
+                uint32_t w[kLDCand];
+#pragma unroll
+                for (uint32_t j = 0; j < kLDCand; j++) w[j] = ld_hdr(dat, blen, p + (lane + 64u * j) * L);
+                const LCDecision d0 = lc_decide(blen - p, eof, __builtin_amdgcn_readfirstlane(w[0]));  // lane 0: the header at p
                 if (d0.kind == 0) break;  // the block's trailer: no event
                 if (d0.stop) {
                     if (lane == 0) hl[n] = (uint16_t)p;
                     n++;
                     break;
                 }
-                const uint32_t L = 7u + d0.length, cand = p + lane * L;
-                bool ok = lane == 0;
-                if (lane && cand < blen && blen - cand >= 7) {
-                    const LCDecision dk = lc_decide(blen - cand, eof, lds32u(dat, cand + 3u));
-                    ok = dk.kind == 1u && dk.length == d0.length;
+                const uint32_t L0 = 7u + d0.length;
+                if (L0 != L) {  // a new run: its candidates (a second trip when any is in the block)
+                    L = L0;
+                    if (p + L < blen) {
+#pragma unroll
+                        for (uint32_t j = 0; j < kLDCand; j++) w[j] = ld_hdr(dat, blen, p + (lane + 64u * j) * L);
+                    }
                 }
-                const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
-                const uint32_t m = nok ? (uint32_t)__builtin_ctzll(nok) : 64u;
-                if (lane < m) hl[n + lane] = (uint16_t)cand;
+                uint32_t m = 64u * kLDCand;
+#pragma unroll
+                for (uint32_t j = kLDCand; j-- > 0;) {  // the first candidate that breaks the run
+                    const uint32_t k = lane + 64u * j, cand = p + k * L;
+                    bool ok = k == 0;
+                    if (k && cand < blen && blen - cand >= 7) {
+                        const LCDecision dk = lc_decide(blen - cand, eof, w[j]);
+                        ok = dk.kind == 1u && dk.length == d0.length;
+                    }
+                    const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
+                    if (nok) m = 64u * j + (uint32_t)__builtin_ctzll(nok);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kLDCand; j++)
+                    if (lane + 64u * j < m) hl[n + lane + 64u * j] = (uint16_t)(p + (lane + 64u * j) * L);
                 n += m;
                 p += m * L;
             }
@@ -702,6 +733,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 }
             }
         }
+        LD_T(tw);
         ld_sync();
         LD_T(tc);
         const uint32_t n = s_n;
@@ -735,16 +767,18 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
 #if JL_LD_PROF
         LD_T(te);
         acc[0] += tb - ta;
-        acc[1] += tc - tb;
+        acc[1] += tw - tb2;
+        acc[6] += tc - tw;
         acc[2] += td - tc;
         acc[3] += te - td;
         acc[4] += 1;
+        acc[5] += tb2 - tb;
 #endif
         b = bn;
     }
 #if JL_LD_PROF
     if (t == 0)
-        for (int i = 0; i < 5; i++) atomicAdd(&g_ld_prof[i], (unsigned long long)acc[i]);
+        for (int i = 0; i < 7; i++) atomicAdd(&g_ld_prof[i], (unsigned long long)acc[i]);
 #endif
 }
 
@@ -759,7 +793,7 @@ hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
 }
 
 #if JL_LD_PROF
-// study builds: read (and clear) lc_dense's phase clocks [stage, walk, crc, stash, blocks]
+// study builds: read (and clear) lc_dense's phase clocks [stage, walk, crc, stash, blocks, issue, walk barrier]
 extern "C" int jl_study_ld_prof(unsigned long long *out) {
     static const unsigned long long zero[8] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ld_prof), sizeof(zero)) != hipSuccess) return -1;
