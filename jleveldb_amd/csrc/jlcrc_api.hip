@@ -1389,6 +1389,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         G.n_rounds = A.rstart + jlk::kLCBins;
         G.seed0 = jlmath::slice4_inv(0xffffffffu);
         G.parts = A.parts;
+        G.study = (uint32_t)opt().gv4_variant;  // 0 unless a study build set JL_OPT_GV4_VARIANT
         JL_HIP(gv4_launch(G, st));
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));

@@ -38,7 +38,12 @@ constexpr uint32_t kAuxZBDword = 5648 + 256 * 128;  // jlmath::kAuxZB
 struct LCGeom {
     uint32_t f, K, r, J;
 };
-__device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) { return (K - 1u) * 16u + (d & 15u); }
+#ifndef JL_LC_BIN_NO_D
+#define JL_LC_BIN_NO_D 0  // study: bins by K only (neighbouring records share rounds; epilogue tables per group)
+#endif
+__device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) {
+    return (K - 1u) * 16u + (JL_LC_BIN_NO_D ? 0u : (d & 15u));
+}
 __device__ __forceinline__ LCGeom lc_geom(uint64_t pa, uint32_t n) {
     LCGeom g;
     g.f = (uint32_t)(pa & 127u);
