@@ -404,7 +404,9 @@ struct GPF {
 // fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study),
 // 6 = no step math (the loads, ring and round bookkeeping with a plain XOR per
 // step: the memory side alone; results wrong), 7 = the data of every round from
-// an L2-resident 1 MiB window (the math side alone; results wrong)
+// an L2-resident 1 MiB window (the math side alone; results wrong), 8 = no
+// epilogue math, 9 = no pad / seed handling in the first and last steps (8, 9:
+// per-round cost studies; results wrong)
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
@@ -474,6 +476,13 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             side_c = wv;
             return;
         }
+        if constexpr (VAR == 9) {  // study: first / last steps as plain steps (no pads, no seed)
+            x0 = gstep_x3(ldsG, ce == e0 ? 0u : x0, gl, wv.x);
+            x1 = gstep_x3(ldsG, ce == e0 ? 0u : x1, gl, wv.y);
+            x2 = gstep_x3(ldsG, ce == e0 ? 0u : x2, gl, wv.z);
+            x3 = gstep_x3(ldsG, ce == e0 ? 0u : x3, gl, wv.w);
+            return;
+        }
         const uint32_t f = GV4<MODE>::LOGC ? cv.f : (uint32_t)(cv.p & 127u);
         uint32_t v[4] = {wv.x, wv.y, wv.z, wv.w};
         // byte selectors from the image (kG4SelByte): v_med3 + one LDS read + v_perm per
@@ -529,7 +538,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         const uint32_t d = cv.d;
         const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
         uint32_t st;
-        if constexpr (GV4<MODE>::LOGC) {
+        if constexpr (VAR == 8) {  // study: no epilogue math (the chains XOR-folded as they are)
+            st = group_xor<8>(xor3(x0, x1, x2) ^ x3 ^ col);
+        } else if constexpr (GV4<MODE>::LOGC) {
             // chain j: its pending gap step, then z^-(4 (j + c) + e), in one table
             // (uniform d mod 16; crc_math.hpp build_lds_image_logchunk)
             const uint32_t sm = kLCMB + 512u * (d & 15u);
@@ -745,6 +756,12 @@ hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_
                                A, zero);
         else if (v == 7)
             hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 7>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 8)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 8>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
+                               A, zero);
+        else if (v == 9)
+            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 9>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
                                A, zero);
         else
             hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,

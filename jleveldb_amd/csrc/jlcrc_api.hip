@@ -780,7 +780,7 @@ int jl_set_option(int option, int64_t value) {
         o.fixed_kernel = (int)value;
         return JL_OK;
     case JL_OPT_GV4_VARIANT:
-        if (value < 0 || value > 7) break;
+        if (value < 0 || value > 9) break;
         o.gv4_variant = (int)value;
         return JL_OK;
 #endif
