@@ -400,8 +400,8 @@ struct GPF {
 };
 
 // VAR: 0 = default (nt ring loads), 1 = strict (vmcnt(0) before every ring use:
-// debugging), 2 = ring loads without nt (cache-policy study), 3 = the product loop
-// (r2's whole 8-entry fast turns, retired in r3), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study),
+// debugging), 2 = ring loads without nt (cache-policy study), 3 = whole 8-entry
+// fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study),
 // 6 = no step math (the loads, ring and round bookkeeping with a plain XOR per
 // step: the memory side alone; results wrong), 7 = the data of every round from
 // an L2-resident 1 MiB window (the math side alone; results wrong), 8 = no
@@ -654,67 +654,31 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                      : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)                                           \
                      : "v"(t0_), "v"(u0_), "v"(t1_), "v"(u1_), "v"(t2_), "v"(u2_), "v"(t3_), "v"(u3_));    \
     }
-    // Per-entry path, ONE copy of its bookkeeping (rare entries, the epilogue,
-    // the round switch, the prefetch cursor's setup) for all 8 slots: only the
-    // slot's wait, copy-out and refill are per slot, a switch on the slot index.
-    // r3: with the path inlined once per slot (8 copies of finish / rare / setup)
-    // the kernel was 60-72 KB of code.  The refill address is taken (after the
-    // slot's wait) before the entry is consumed; that only moves the prefetch
-    // cursor's descriptor load (desc_issue) before the compute cursor's round
-    // switch of the same entry, which the set protocol above allows: the compute
-    // cursor read the set being refilled >= 1 entry before (E >= P).
-#define JL_TK(u, RQ, R0, R1, R2, R3)                                                                       \
-    case u:                                                                                                \
-        if constexpr (VAR == 2)                                                                            \
-            asm volatile("v_mov_b32 %0, " R0 "\n\tv_mov_b32 %1, " R1 "\n\tv_mov_b32 %2, " R2               \
-                         "\n\tv_mov_b32 %3, " R3 "\n\tglobal_load_dwordx4 " RQ ", %4, off"                 \
-                         : "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3)                                      \
-                         : "v"(a_)                                                                         \
-                         : "memory", R0, R1, R2, R3);                                                      \
-        else                                                                                               \
-            asm volatile("v_mov_b32 %0, " R0 "\n\tv_mov_b32 %1, " R1 "\n\tv_mov_b32 %2, " R2               \
-                         "\n\tv_mov_b32 %3, " R3 "\n\tglobal_load_dwordx4 " RQ ", %4, off nt"              \
-                         : "=&v"(w0), "=&v"(w1), "=&v"(w2), "=&v"(w3)                                      \
-                         : "v"(a_)                                                                         \
-                         : "memory", R0, R1, R2, R3);                                                      \
-        break;
-    // one entry of slot u on the per-entry path; false when the wave is done
-    // The slot's wait comes FIRST: the prefetch cursor's setup (inside pf.next)
-    // reads a pinned descriptor set whose load only a ring wait retires (r3: with
-    // the wait after pf.next, a wave whose first round has 9 entries read its next
-    // round's set at step 0, before any wait: garbage addresses, a GPU fault)
-    auto entry = [&](uint32_t u) -> bool {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");
-        const uint64_t a_ = pf.next(A, lane);
-        uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        switch (u) { JL_GV4_SLOTS(JL_TK) }
-        if (ce > e0 && ce + 1u < cE) {
-            if constexpr (VAR == 6) {
-                x0 ^= w0;
-                x1 ^= w1;
-                x2 ^= w2;
-                x3 ^= w3;
-            } else {
-                x0 = gstep_x3(ldsG, x0, gl, w0);
-                x1 = gstep_x3(ldsG, x1, gl, w1);
-                x2 = gstep_x3(ldsG, x2, gl, w2);
-                x3 = gstep_x3(ldsG, x3, gl, w3);
-            }
-        } else {
-            v4u wv_;
-            wv_.x = w0;
-            wv_.y = w1;
-            wv_.z = w2;
-            wv_.w = w3;
-            rare(wv_);
-        }
-        return !(++ce == cE && !finish());
-    };
+#define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
+    {                                                                                                      \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
+        if (ce > e0 && ce + 1u < cE) {                                                                     \
+            JL_XS4(R0, R1, R2, R3)                                                                         \
+        } else {                                                                                           \
+            v4u wv_;                                                                                       \
+            uint32_t w0_, w1_, w2_, w3_;                                                                   \
+            asm volatile("v_mov_b32 %0, " R0 "\n\tv_mov_b32 %1, " R1 "\n\tv_mov_b32 %2, " R2                   \
+                         "\n\tv_mov_b32 %3, " R3                                                            \
+                         : "=v"(w0_), "=v"(w1_), "=v"(w2_), "=v"(w3_));                                     \
+            wv_.x = w0_;                                                                                   \
+            wv_.y = w1_;                                                                                   \
+            wv_.z = w2_;                                                                                   \
+            wv_.w = w3_;                                                                                   \
+            rare(wv_);                                                                                     \
+        }                                                                                                  \
+        if (++ce == cE && !finish()) break;                                                                \
+        JL_LOAD(RQ, R0, R1, R2, R3)                                                                        \
+    }
     // Fast half turn: the next 4 entries of BOTH cursors are plain steps of their
     // current rounds (no rare entry, no epilogue, no round switch), so they run
     // as straight-line code: wait, the 4 chains, and the refill at the cursor's
-    // address + 128 (u mod 4) — no per-step bookkeeping.  Otherwise one entry
-    // takes the per-entry path (half turns start on slot 0 or 4 only).
+    // address + 128 (u mod 4) — no per-step bookkeeping.  Otherwise the half
+    // takes the per-entry path (either way it ends on the next half's slot).
     // Half turns rather than whole 8-entry turns: a round boundary then blocks
     // fewer entries from the fast path (rounds of 32 entries: ~72 % fast vs ~47 %).
 #define JL_F(u, RQ, R0, R1, R2, R3)                                                                        \
@@ -724,32 +688,38 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         JL_GLD(RQ, pf.addr, 128 * ((u) & 3), R0, R1, R2, R3)                                               \
     }
     const bool fast_ok = !DBG && VAR != 5;  // debugging / study variants: per-entry path only
-#define JL_HALF_OK (fast_ok && ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E)
-#define JL_HALF_DONE                                                                                       \
-    ce = uni(ce + 4u);                                                                                     \
-    pf.e = uni(pf.e + 4u);                                                                                 \
-    pf.addr += 512u;
-    uint32_t u = 0;  // the next entry's slot (wave-uniform)
-    for (;;) {
-        if (u == 0u && JL_HALF_OK) {
-            JL_GV4_SLOTS_LO(JL_F)
-            JL_HALF_DONE
-            u = 4u;
-            continue;
-        }
-        if (u == 4u && JL_HALF_OK) {
-            JL_GV4_SLOTS_HI(JL_F)
-            JL_HALF_DONE
-            u = 0u;
-            continue;
-        }
-        if (!entry(u)) break;
-        u = uni((u + 1u) & 7u);
+#define JL_HALF(SLOTS)                                                                                     \
+    if (fast_ok && ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E) {             \
+        SLOTS(JL_F)                                                                                        \
+        ce = uni(ce + 4u);                                                                                 \
+        pf.e = uni(pf.e + 4u);                                                                             \
+        pf.addr += 512u;                                                                                   \
+    } else {                                                                                               \
+        SLOTS(JL_G)                                                                                        \
     }
-#undef JL_HALF_OK
-#undef JL_HALF_DONE
-#undef JL_TK
+    if constexpr (VAR == 3) {  // study: whole 8-entry fast turns only
+        for (;;) {
+            if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
+                pf.e + (uint32_t)P_ < pf.E) {
+                JL_GV4_SLOTS_LO(JL_F)
+                pf.addr += 512u;
+                JL_GV4_SLOTS_HI(JL_F)
+                ce = uni(ce + (uint32_t)P_);
+                pf.e = uni(pf.e + (uint32_t)P_);
+                pf.addr += 512u;
+                continue;
+            }
+            JL_GV4_SLOTS(JL_G)
+        }
+    } else {
+        for (;;) {
+            JL_HALF(JL_GV4_SLOTS_LO)
+            JL_HALF(JL_GV4_SLOTS_HI)
+        }
+    }
+#undef JL_HALF
 #undef JL_F
+#undef JL_G
 #undef JL_XS4
 #undef JL_LK
 #undef JL_LOAD
