@@ -21,7 +21,7 @@ if os.environ.get("GV4_VARIANT"):  # study build (JLCRC_STUDY_LIB): general_v4.h
     jl.set_option(jl.OPT_GV4_VARIANT, int(os.environ["GV4_VARIANT"]))
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream()
-if which in ("all", "c3"):
+if which == "all" or "c3" in which.split(","):
     print(json.dumps(bench.secondary_c3(dev, stream, steps, 3, cpu=False)), flush=True)
     torch.cuda.empty_cache()
 if which in ("all", "dispatch"):
