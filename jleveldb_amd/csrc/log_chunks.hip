@@ -87,9 +87,40 @@ typedef uint64_t __attribute__((aligned(1))) u64u;
 // Header bytes 0..6 at p ([crc 0..3][len lo][len hi][type]) as one 8-byte load
 // when 8 bytes are left in the block (one memory request on the walk's serial
 // chain), else two dword loads.
+// Cache policy of lc_walk's header hops: 1 = nt (the product), 0 = the default
+// policy, 2 = sc1, 3 = sc0 sc1, 4 = sc0 sc1 nt (study builds).  r3 same-box A/B
+// (tools/ab_libs.sh, 3 rounds): C5 1 056-B 1.034 -> 1.011 ms with nt (and with
+// sc0 sc1 nt), mixed and DBBench unchanged within noise; sc1 / sc0 sc1 alone no
+// change.  The walk's random header lines are not re-read soon (the rounds read
+// the records much later), so they should not displace L2-resident lines.
+#ifndef JL_LC_HDR_POLICY
+#define JL_LC_HDR_POLICY 1
+#endif
 __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
     if (rem >= 8) return *(const u64u *)p;
     return (uint64_t)ld_u32u(p) | ((uint64_t)(ld_u32u(p + 3) >> 8) << 32);
+}
+// the walk's hop load (lc_walk): lc_header's bytes with JL_LC_HDR_POLICY (an asm load,
+// waited for at once: the hop is a dependent chain anyway)
+__device__ __forceinline__ uint64_t lc_hop(const uint8_t *p, uint64_t rem) {
+#if JL_LC_HDR_POLICY
+    if (rem >= 8) {
+        uint64_t v;
+#if JL_LC_HDR_POLICY == 1
+#define JL_HP " nt"
+#elif JL_LC_HDR_POLICY == 2
+#define JL_HP " sc1"
+#elif JL_LC_HDR_POLICY == 3
+#define JL_HP " sc0 sc1"
+#else
+#define JL_HP " sc0 sc1 nt"
+#endif
+        asm volatile("global_load_dwordx2 %0, %1, off" JL_HP "\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+#undef JL_HP
+        return v;
+    }
+#endif
+    return lc_header(p, rem);
 }
 
 // Adds one (s = 1) or removes one (s = ~0u) record of geometry g to the chunk
@@ -136,7 +167,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         const bool eof = be - bs < 32768u;
         const uint64_t base = (uint64_t)(uintptr_t)A.log;
         uint64_t p = bs;
-        uint64_t hv = be - p >= 7 ? lc_header(A.log + p, be - p) : 0;
+        uint64_t hv = be - p >= 7 ? lc_hop(A.log + p, be - p) : 0;
         bool dense = false;
         for (;;) {
             const LCDecision d = lc_decide(be - p, eof, (uint32_t)(hv >> 24));
@@ -148,7 +179,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
             }
             const uint64_t pn = p + 7u + d.length;
             const uint32_t stored = (uint32_t)hv;
-            if (!d.stop && be - pn >= 7) hv = lc_header(A.log + pn, be - pn);
+            if (!d.stop && be - pn >= 7) hv = lc_hop(A.log + pn, be - pn);
             const uint64_t slot = d.length | (d.type << 16) | (d.kind << 24) | ((uint64_t)stored << 32);
             if (cnt < kLCLdsSlots) ls[threadIdx.x][cnt] = slot;
             else A.slots[b * kLCSlots + cnt] = slot;
