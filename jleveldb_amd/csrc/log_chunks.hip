@@ -102,6 +102,31 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
 }
 // the walk's hop load (lc_walk): lc_header's bytes with JL_LC_HDR_POLICY (an asm load,
 // waited for at once: the hop is a dependent chain anyway)
+// Study switches (0 in the product): non-temporal stores of the events / round
+// descriptors / stash and loads of the stash (JL_NT_EV), and lc_dense's block
+// staging loads (JL_NT_STAGE).  r3 same-box A/B (tools/ab_libs.sh, C5 sets
+// mixed / 1 056-B / DBBench, ms): product 0.82 / 1.014 / 1.59, JL_NT_EV 0.825 /
+// 1.035 / 1.587 (gv4 then reads its descriptors from HBM), JL_NT_STAGE 0.826 /
+// 1.02 / 1.62, both 0.845 / 1.032 / 1.588: not kept.
+#ifndef JL_NT_EV
+#define JL_NT_EV 0
+#endif
+#ifndef JL_NT_STAGE
+#define JL_NT_STAGE 0
+#endif
+typedef uint32_t lc_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lc_st16(void *p, lc_v4 v) {
+    if (JL_NT_EV) __builtin_nontemporal_store(v, (lc_v4 *)p);
+    else *(lc_v4 *)p = v;
+}
+__device__ __forceinline__ void lc_st8(uint64_t *p, uint64_t v) {
+    if (JL_NT_EV) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ uint64_t lc_ld8(const uint64_t *p) {
+    if (JL_NT_EV) return __builtin_nontemporal_load(p);
+    return *p;
+}
 __device__ __forceinline__ uint64_t lc_hop(const uint8_t *p, uint64_t rem) {
 #if JL_LC_HDR_POLICY
     if (rem >= 8) {
@@ -265,11 +290,8 @@ __device__ __forceinline__ void lc_desc(const LCArgs &A, const uint32_t *rs, uin
                                         uint32_t seed, uint32_t d, uint32_t idx, uint32_t stored) {
     const uint64_t round = (uint64_t)rs[lc_bin(K, d)] + rank / 8u;
     if (round >= A.round_cap) return;  // cap_flag is set (lc_setup)
-    GDesc g;
-    g.pd = (prel & 0xffffffffffull) | ((uint64_t)K << 40) | ((uint64_t)seed << 48) | ((uint64_t)d << 56);
-    g.idx = idx;
-    g.K = stored;
-    A.desc[round * 8u + rank % 8u] = g;
+    const uint64_t pd = (prel & 0xffffffffffull) | ((uint64_t)K << 40) | ((uint64_t)seed << 48) | ((uint64_t)d << 56);
+    lc_st16(&A.desc[round * 8u + rank % 8u], lc_v4{(uint32_t)pd, (uint32_t)(pd >> 32), idx, stored});
 }
 
 __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v);
@@ -340,13 +362,8 @@ __device__ __forceinline__ void lc_place_wave(const LCArgs &A, uint32_t *ctr, co
 __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t off, uint32_t length, uint32_t type,
                                          uint32_t kind) {
     if (at >= A.ev_cap) return;
-    LogEvent e;
-    e.offset = off;
-    e.length = length;
-    e.type = (uint8_t)type;
-    e.kind = (uint8_t)kind;
-    e.pad = 0;
-    A.ev[at] = e;
+    // LogEvent {u64 offset, u32 length, u8 type, u8 kind, u16 pad}
+    lc_st16(&A.ev[at], lc_v4{(uint32_t)off, (uint32_t)(off >> 32), length, (type & 0xffu) | ((kind & 0xffu) << 8)});
 }
 
 // A workgroup builds the kLCGroup blocks one walk wave counted (their rank
@@ -413,7 +430,7 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         if (doff != kLCNotDense) {  // dense block: its events from the stash (lc_dense)
             if (doff == ~0ull) continue;  // did not fit: the event array is too small anyway
             for (uint32_t k = lane; k < cnt[i]; k += 64u) {
-                const uint64_t e = A.stash[doff + k];
+                const uint64_t e = lc_ld8(&A.stash[doff + k]);
                 lc_event(A, st[i] + k, b * 32768u + (e & 0xffffu), (uint32_t)(e >> 16) & 0xffffu,
                          (uint32_t)(e >> 32) & 0xffu, (uint32_t)(e >> 40) & 0xffu);
             }
@@ -622,14 +639,25 @@ struct LDPre {
     ld_v4 a, b, c, d, e, f, g, h;
     __device__ __forceinline__ void load(const uint8_t *blk, uint32_t t) {
         const ld_v4 *s = (const ld_v4 *)blk + t;
-        a = s[0 * kLDThreads];
-        b = s[1 * kLDThreads];
-        c = s[2 * kLDThreads];
-        d = s[3 * kLDThreads];
-        e = s[4 * kLDThreads];
-        f = s[5 * kLDThreads];
-        g = s[6 * kLDThreads];
-        h = s[7 * kLDThreads];
+        if (JL_NT_STAGE) {
+            a = __builtin_nontemporal_load(s + 0 * kLDThreads);
+            b = __builtin_nontemporal_load(s + 1 * kLDThreads);
+            c = __builtin_nontemporal_load(s + 2 * kLDThreads);
+            d = __builtin_nontemporal_load(s + 3 * kLDThreads);
+            e = __builtin_nontemporal_load(s + 4 * kLDThreads);
+            f = __builtin_nontemporal_load(s + 5 * kLDThreads);
+            g = __builtin_nontemporal_load(s + 6 * kLDThreads);
+            h = __builtin_nontemporal_load(s + 7 * kLDThreads);
+        } else {
+            a = s[0 * kLDThreads];
+            b = s[1 * kLDThreads];
+            c = s[2 * kLDThreads];
+            d = s[3 * kLDThreads];
+            e = s[4 * kLDThreads];
+            f = s[5 * kLDThreads];
+            g = s[6 * kLDThreads];
+            h = s[7 * kLDThreads];
+        }
     }
     __device__ __forceinline__ void store(uint32_t *dat, uint32_t t) const {
         ld_v4 *d4 = (ld_v4 *)dat + t;
@@ -798,7 +826,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 const uint32_t h = hl[r];
                 const LCDecision d = lc_decide(blen - h, eof, blen - h >= 7 ? lds32u(dat, h + 3u) : 0u);
                 const uint64_t kind = r == bad ? 2u : (bad != kLCNone && r > bad ? 0u : d.kind);
-                A.stash[so + r] = h | ((uint64_t)d.length << 16) | ((uint64_t)d.type << 32) | (kind << 40);
+                lc_st8(&A.stash[so + r], h | ((uint64_t)d.length << 16) | ((uint64_t)d.type << 32) | (kind << 40));
             }
 #if JL_LD_PROF
         LD_T(te);
