@@ -429,10 +429,22 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         const uint64_t doff = A.dense_off[b];
         if (doff != kLCNotDense) {  // dense block: its events from the stash (lc_dense)
             if (doff == ~0ull) continue;  // did not fit: the event array is too small anyway
-            for (uint32_t k = lane; k < cnt[i]; k += 64u) {
-                const uint64_t e = lc_ld8(&A.stash[doff + k]);
-                lc_event(A, st[i] + k, b * 32768u + (e & 0xffffu), (uint32_t)(e >> 16) & 0xffffu,
-                         (uint32_t)(e >> 32) & 0xffu, (uint32_t)(e >> 40) & 0xffu);
+            // 4 loads in flight per lane before the stores (the compiler cannot move a
+            // stash load above an event store: it does not know they do not alias)
+            for (uint32_t k0 = 0; k0 < cnt[i]; k0 += 256u) {
+                uint64_t e[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t k = k0 + lane + 64u * j;
+                    e[j] = k < cnt[i] ? lc_ld8(&A.stash[doff + k]) : 0ull;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 4; j++) {
+                    const uint32_t k = k0 + lane + 64u * j;
+                    if (k < cnt[i])
+                        lc_event(A, st[i] + k, b * 32768u + (e[j] & 0xffffu), (uint32_t)(e[j] >> 16) & 0xffffu,
+                                 (uint32_t)(e[j] >> 32) & 0xffu, (uint32_t)(e[j] >> 40) & 0xffu);
+                }
             }
             continue;
         }
