@@ -89,7 +89,7 @@ typedef uint64_t __attribute__((aligned(1))) u64u;
 // chain), else two dword loads.
 // Cache policy of lc_walk's header hops: 1 = nt (the product), 0 = the default
 // policy, 2 = sc1, 3 = sc0 sc1, 4 = sc0 sc1 nt (study builds).  r3 same-box A/B
-// (tools/ab_libs.sh, 3 rounds): C5 1 056-B 1.034 -> 1.011 ms with nt (and with
+// (tools/ab_lib.sh, 3 rounds): C5 1 056-B 1.034 -> 1.011 ms with nt (and with
 // sc0 sc1 nt), mixed and DBBench unchanged within noise; sc1 / sc0 sc1 alone no
 // change.  The walk's random header lines are not re-read soon (the rounds read
 // the records much later), so they should not displace L2-resident lines.
@@ -104,7 +104,7 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
 // waited for at once: the hop is a dependent chain anyway)
 // Study switches (0 in the product): non-temporal stores of the events / round
 // descriptors / stash and loads of the stash (JL_NT_EV), and lc_dense's block
-// staging loads (JL_NT_STAGE).  r3 same-box A/B (tools/ab_libs.sh, C5 sets
+// staging loads (JL_NT_STAGE).  r3 same-box A/B (tools/ab_lib.sh, C5 sets
 // mixed / 1 056-B / DBBench, ms): product 0.82 / 1.014 / 1.59, JL_NT_EV 0.825 /
 // 1.035 / 1.587 (gv4 then reads its descriptors from HBM), JL_NT_STAGE 0.826 /
 // 1.02 / 1.62, both 0.845 / 1.032 / 1.588: not kept.
