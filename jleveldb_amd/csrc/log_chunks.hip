@@ -559,6 +559,11 @@ constexpr uint32_t kLDCand = JL_LD_CAND;  // walk candidates per lane and LDS tr
 #ifndef JL_LD_REP
 #define JL_LD_REP 1
 #endif
+#ifndef JL_LD_HLCAP
+#define JL_LD_HLCAP kLDMaxEv  // study: a smaller header buffer (only for logs of <= this many events per block)
+#endif
+// r3 (JL_LD_HLCAP 2048 keeps 3 workgroups per CU with 2 table copies): DBBench set
+// 1.561 ms (product) vs 1.645 (2 copies, 3 per CU) and 2.00 (4 copies, 2 per CU)
 // Slicing width: a record's dwords go round-robin to kLDSlice / 4 independent
 // chains, each advancing kLDSlice bytes per step through T_{S-1}..T_{S-4}, so the
 // dependent LDS round trips per record drop from one per 4 B to one per S bytes
@@ -707,7 +712,7 @@ __device__ unsigned long long g_ld_prof[8];
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];          // the block (+ zero pad: header reads near its end)
     __shared__ uint32_t tab[kLDSlice * 256 * kLDRep];  // T_k[e] copy r at word (256 k + e) kLDRep + r
-    __shared__ uint16_t hl[kLDMaxEv];           // header offsets of the block's events
+    __shared__ uint16_t hl[JL_LD_HLCAP];        // header offsets of the block's events
     __shared__ uint32_t s_n, s_bad;
     __shared__ unsigned long long s_off;
     const uint32_t t = threadIdx.x, lane = t & 63u, rep = t % kLDRep;
@@ -860,7 +865,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + kLDSlice * 256 * kLDRep * 4 + kLDMaxEv * 2 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + kLDSlice * 256 * kLDRep * 4 + JL_LD_HLCAP * 2 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
