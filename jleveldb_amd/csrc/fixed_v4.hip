@@ -38,6 +38,10 @@
 
 #include "engine_device.hpp"
 
+#ifndef JL_RING_SLACK
+#define JL_RING_SLACK 2  // see general_v4.hip
+#endif
+
 #ifndef JL_STUDY
 #define JL_STUDY 0
 #endif
@@ -105,7 +109,7 @@ struct V4Wave {
     template <int K>
     __device__ __forceinline__ void step() {
         constexpr int SL = K % Gm::P;
-        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[SL]) : "n"(Gm::P - 2));
+        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[SL]) : "n"(Gm::P - JL_RING_SLACK));
         if (K == 0) {  // real XORs (zero is opaque): a plain copy here lets RA copy the ring slot before its wait
             x0 = s_init ^ w[SL].x;
             x1 = zero ^ w[SL].y;

@@ -131,6 +131,16 @@ constexpr uint32_t kLCMB = 16384, kLCSelB = 30720;
 #error "JL_GV4_THREADS: 512 or 1024"
 #endif
 #define JL_GV4_RING 8
+// A ring use waits vmcnt(P - JL_RING_SLACK).  s_waitcnt vmcnt(N) leaves the N
+// youngest vector-memory operations of any kind in flight, in issue order, so
+// P - 1 would be exact for gv4; r3 same-box A/B with slack 1 (7 loads in flight
+// instead of 6): C3 2.055 / 2.065 vs 2.059 / 2.06 ms, C5 1 056-B and mixed
+// unchanged, so 2 stays (the 4 KiB kernel's ring also fails the dataflow check
+// of tools/asm_ring_check.py at slack 1: a compiler copy of a slot sits before
+// the wait that would then cover it).
+#ifndef JL_RING_SLACK
+#define JL_RING_SLACK 2
+#endif
 
 template <int MODE>
 struct GV4 {
@@ -656,7 +666,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     }
 #define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - JL_RING_SLACK) : "memory");                         \
         if (ce > e0 && ce + 1u < cE) {                                                                     \
             JL_XS4(R0, R1, R2, R3)                                                                         \
         } else {                                                                                           \
@@ -683,7 +693,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     // fewer entries from the fast path (rounds of 32 entries: ~72 % fast vs ~47 %).
 #define JL_F(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - 2) : "memory");                         \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - JL_RING_SLACK) : "memory");                         \
         JL_XS4(R0, R1, R2, R3)                                                                             \
         JL_GLD(RQ, pf.addr, 128 * ((u) & 3), R0, R1, R2, R3)                                               \
     }
