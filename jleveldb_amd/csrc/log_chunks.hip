@@ -543,7 +543,10 @@ __device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uin
     return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
 }
 #ifndef JL_LD_CAND
-#define JL_LD_CAND 1  // r3n A/B (DBBench set): 1 1.62 ms, 2 1.64, 4 1.73 (more LDS reads per trip)
+#define JL_LD_CAND 1  // r3n A/B (DBBench set): 1 1.62 ms, 2 1.64, 4 1.73 (more LDS reads per trip);
+                      // r3: speculating after a lone record on the last long run's stride
+                      // (kept across blocks) 1.589 vs 1.575 ms: a first trip of 64 distinct
+                      // reads instead of one broadcast costs more than the reload it saves
 #endif
 constexpr uint32_t kLDCand = JL_LD_CAND;  // walk candidates per lane and LDS trip
 
