@@ -44,6 +44,32 @@ struct LCGeom {
 __device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) {
     return (K - 1u) * 16u + (JL_LC_BIN_NO_D ? 0u : (d & 15u));
 }
+#ifndef JL_LC_ILV
+#define JL_LC_ILV 0  // study: the rounds of one K j-major over its 16 d bins (see lc_round)
+#endif
+static_assert(!(JL_LC_ILV && JL_LC_BIN_NO_D), "JL_LC_ILV needs the d bins");
+// Round of the j-th round of bin (K, d).  Default: the bins' rounds in bin
+// order.  JL_LC_ILV: the rounds of one K interleaved over its 16 d bins (round j
+// of every bin, then round j + 1), so that neighbouring records of a stream of
+// similar lengths (which cycle through the d bins) sit in adjacent rounds, i.e.
+// on one XCD at about the same time, and their shared boundary lines come from
+// L2.  rs: kLCBins + 1 round starts (saturating: the total is clamped past the
+// descriptor capacity).
+__device__ __forceinline__ uint64_t lc_round(const uint32_t *rs, uint32_t K, uint32_t d, uint32_t j) {
+#if JL_LC_ILV
+    const uint32_t b0 = (K - 1u) * 16u, dd = d & 15u;
+    uint32_t pos = rs[b0];
+#pragma unroll
+    for (uint32_t e = 0; e < 16u; e++) {
+        const uint32_t a = rs[b0 + e], z = rs[b0 + e + 1u];
+        const uint32_t nr = z > a ? z - a : 0u;
+        pos += (nr < j ? nr : j) + (e < dd && nr > j ? 1u : 0u);
+    }
+    return pos;
+#else
+    return (uint64_t)rs[lc_bin(K, d)] + j;
+#endif
+}
 __device__ __forceinline__ LCGeom lc_geom(uint64_t pa, uint32_t n) {
     LCGeom g;
     g.f = (uint32_t)(pa & 127u);
@@ -279,8 +305,20 @@ __global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
         A.rstart[kLCBins] = over ? (uint32_t)A.round_cap : total;
         if (over) atomicOr(A.cap_flag, 1u);
     }
+#if JL_LC_ILV
+    uint64_t r = (uint32_t)__shfl((int)ex, (int)(lane & ~15u));  // the K's first round
+    {
+        const uint32_t j = cnt / 8u, dd = lane & 15u;
+#pragma unroll
+        for (uint32_t e = 0; e < 16u; e++) {
+            const uint32_t nr = (uint32_t)__shfl((int)rounds, (int)((lane & ~15u) + e));
+            r += (nr < j ? nr : j) + (e < dd && nr > j ? 1u : 0u);
+        }
+    }
+#else
+    const uint64_t r = (uint64_t)ex + cnt / 8u;
+#endif
     if (cnt & 7u) {
-        const uint64_t r = (uint64_t)ex + cnt / 8u;
         if (r < A.round_cap)
             for (uint32_t g = cnt & 7u; g < 8u; g++) A.desc[r * 8u + g].idx = kGNull;
     }
@@ -288,7 +326,7 @@ __global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
 
 __device__ __forceinline__ void lc_desc(const LCArgs &A, const uint32_t *rs, uint32_t K, uint32_t rank, uint64_t prel,
                                         uint32_t seed, uint32_t d, uint32_t idx, uint32_t stored) {
-    const uint64_t round = (uint64_t)rs[lc_bin(K, d)] + rank / 8u;
+    const uint64_t round = lc_round(rs, K, d, rank / 8u);
     if (round >= A.round_cap) return;  // cap_flag is set (lc_setup)
     const uint64_t pd = (prel & 0xffffffffffull) | ((uint64_t)K << 40) | ((uint64_t)seed << 48) | ((uint64_t)d << 56);
     lc_st16(&A.desc[round * 8u + rank % 8u], lc_v4{(uint32_t)pd, (uint32_t)(pd >> 32), idx, stored});
@@ -400,11 +438,11 @@ __device__ __forceinline__ void lc_finish(const LCArgs &A) {
 }
 
 __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) {
-    __shared__ uint32_t ctr[kLCCounters], rs[kLCBins];
+    __shared__ uint32_t ctr[kLCCounters], rs[kLCBins + 1];
     const uint64_t nw = A.n_grp;
     for (uint32_t i = threadIdx.x; i < kLCCounters; i += blockDim.x)
         ctr[i] = A.checksum ? A.hscan[i * nw + blockIdx.x] - A.hscan[i * nw] : 0u;
-    for (uint32_t i = threadIdx.x; i < kLCBins && A.checksum; i += blockDim.x) rs[i] = A.rstart[i];
+    for (uint32_t i = threadIdx.x; i <= kLCBins && A.checksum; i += blockDim.x) rs[i] = A.rstart[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // the wave's blocks wv, wv + 16, ... of the group: all their loads first
