@@ -553,6 +553,7 @@ def main():
     per_launch = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)]
     kern_ms = sum(per_launch) / args.steps
     wall = shd.job_wall_time(wall, dev)  # max over ranks (no-op at N=1)
+    rank_kern = shd.per_rank(kern_ms, dev)  # every rank's kernel ms (HIP events), beside the MAX
     if args.strong_total:
         value = args.strong_total * 4096 * args.steps / wall / GIB
     else:
@@ -594,6 +595,8 @@ def main():
                        "blocks_per_gpu": n, "block_bytes": 4096,
                        "parallelism": f"shard{world}" + (" (same-device rehearsal, gloo)" if args.same_device else "")},
             "result_allgather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "rank_kernel_ms": [round(x, 4) for x in rank_kern],
+            "rank_kernel_ms_spread": round(max(rank_kern) - min(rank_kern), 4),
             "parity_gathered_vs_single_launch": parity,
             "roofline": {
                 "bound": "hbm",

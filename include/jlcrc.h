@@ -102,7 +102,7 @@ const char *jl_version(void);
  *                            (one table)
  *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
  *                            default 12 MiB (one WAL)
- * Study builds only (make STUDY=1): JL_OPT_FIXED_KERNEL, JL_OPT_GV4_VARIANT. */
+ * Study builds only (make STUDY=1): JL_OPT_GV4_VARIANT (crc_gv4_kernel bound-study variants). */
 #define JL_OPT_GENERAL_PATH 1
 #define JL_OPT_STREAM_DEPTH 2
 #define JL_OPT_STREAM_PARTITION 3
@@ -111,7 +111,6 @@ const char *jl_version(void);
 #define JL_OPT_STAGE_THREADS 6
 #define JL_OPT_HOST_THRESHOLD 7
 #define JL_OPT_LOG_HOST_THRESHOLD 8
-#define JL_OPT_FIXED_KERNEL 100
 #define JL_OPT_GV4_VARIANT 101
 #define JL_PATH_AUTO 0
 #define JL_PATH_STREAM 1

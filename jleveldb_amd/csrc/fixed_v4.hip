@@ -42,10 +42,6 @@
 #define JL_RING_SLACK 2  // see general_v4.hip
 #endif
 
-#ifndef JL_STUDY
-#define JL_STUDY 0
-#endif
-
 namespace jlk {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -203,42 +199,13 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
 }
 
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
-                             int grid, int lpb, int nt, int shape, hipStream_t st) {
+                             int grid, hipStream_t st) {
     // the product kernel: 8 lanes per block, nt loads, 8-slot ring, 1024 threads
-    // (r1 sustained A/B: 0.638 ms vs 0.643 for the 16-slot ring, 0.654 at 512 threads)
-    if (lpb == 8 && nt && shape == 3) {
-        hipLaunchKernelGGL((crc_fixed4k_v4_kernel<8, true, 8, 1024>), dim3(grid), dim3(1024), 0, st,
-                           (const uint4 *)img, data, n_blocks, flags, out);
-        return hipGetLastError();
-    }
-#if JL_STUDY
-#define JL_V4(L, N)                                                                                                 \
-    hipLaunchKernelGGL((crc_fixed4k_v4_kernel<L, N>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, \
-                       n_blocks, flags, out)
-#define JL_V4S(R, T)                                                                                                \
-    hipLaunchKernelGGL((crc_fixed4k_v4_kernel<8, true, R, T>), dim3(grid), dim3(T), 0, st, (const uint4 *)img, \
-                       data, n_blocks, flags, out)
-    // occupancy / ring-depth study shapes (ring slots, threads per CU): 1 = (8, 512), 2 = (16, 512)
-    if (shape == 1) JL_V4S(8, 512);
-    else if (shape == 2) JL_V4S(16, 512);
-    if (shape) return hipGetLastError();
-#undef JL_V4S
-    if (lpb == 8) {
-        if (nt) JL_V4(8, true);
-        else JL_V4(8, false);
-    } else if (lpb == 16) {
-        JL_V4(16, true);
-    } else {
-        return hipErrorInvalidValue;
-    }
-#undef JL_V4
+    // (r1 sustained A/B: 0.638 ms vs 0.643 for the 16-slot ring, 0.654 at 512 threads;
+    // the other shapes live on the branch study-superseded-kernels)
+    hipLaunchKernelGGL((crc_fixed4k_v4_kernel<8, true, 8, 1024>), dim3(grid), dim3(1024), 0, st,
+                       (const uint4 *)img, data, n_blocks, flags, out);
     return hipGetLastError();
-#else
-    (void)lpb;
-    (void)nt;
-    (void)shape;
-    return hipErrorInvalidValue;
-#endif
 }
 
 }  // namespace jlk

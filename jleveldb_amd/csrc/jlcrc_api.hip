@@ -226,7 +226,6 @@ struct Options {
     int stage_threads = 8;            // JL_OPT_STAGE_THREADS: host threads copying into pinned staging
     int64_t host_threshold = kHostThresholdDefault;  // JL_OPT_HOST_THRESHOLD: smaller host-memory calls run on the host
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
-    int fixed_kernel = 7;             // study: JL_OPT_FIXED_KERNEL (7 = the v4 product kernel)
     int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
 };
 Options &opt() {
@@ -551,21 +550,6 @@ static uint64_t *make_partition(const jlk::KParams &P, uint64_t waves, hipStream
         *rc = fail(JL_ERR_HIP, "partition failed");
         return nullptr;
     }
-#if JL_STUDY
-    if (getenv("JL_PARTITION_DUMP")) {  // debugging: range sizes of the partition
-        std::vector<uint64_t> h(waves + 1), hi(P.n);
-        (void)hipMemcpyAsync(h.data(), part, (waves + 1) * 8, hipMemcpyDeviceToHost, st);
-        (void)hipMemcpyAsync(hi.data(), incl, P.n * 8, hipMemcpyDeviceToHost, st);
-        (void)hipStreamSynchronize(st);
-        uint64_t mx = 0, mn = ~0ull, bad = 0;
-        for (uint64_t w = 0; w < waves; w++) {
-            if (h[w + 1] < h[w]) bad++;
-            else { mx = std::max(mx, h[w + 1] - h[w]); mn = std::min(mn, h[w + 1] - h[w]); }
-        }
-        fprintf(stderr, "partition n=%llu waves=%llu min=%llu max=%llu bad=%llu\n", (unsigned long long)P.n,
-                (unsigned long long)waves, (unsigned long long)mn, (unsigned long long)mx, (unsigned long long)bad);
-    }
-#endif
     return part;  // == buf + incl_bytes; freed through free_partition
 }
 
@@ -647,33 +631,8 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     A.parts = parts;
     A.desc = desc;
     A.n_rounds = n_rounds;
-#if JL_STUDY
-    unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
-    if (const char *dbg = getenv("JL_GV4_DEBUG")) {  // "lo:hi" valid load range (hex), debugging only
-        A.P.dbg_lo = strtoull(dbg, nullptr, 16);
-        const char *c = strchr(dbg, ':');
-        A.P.dbg_hi = c ? strtoull(c + 1, nullptr, 16) : ~0ull;
-        if (e == hipSuccess) e = hipMalloc((void **)&d_dbg, sizeof(h_dbg));
-        if (e == hipSuccess) e = hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st);
-        A.P.dbg = d_dbg;
-        A.study = 4;
-    }
-#endif
     if (e == hipSuccess) e = gv4_launch(A, st);
     if (e == hipSuccess && SP.part_cap) e = jlk::launch_gv4_combine(P, SP, parts, st);
-#if JL_STUDY
-    if (d_dbg) {
-        uint32_t hr = 0;
-        if (e == hipSuccess) e = hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(&hr, n_rounds, 4, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        (void)hipFree(d_dbg);
-        fprintf(stderr, "JL_GV4_DEBUG mode=%d n=%llu rounds=%u bad=%llu\n", P.mode, (unsigned long long)P.n, hr, h_dbg[0]);
-        for (unsigned long long i = 0; i < h_dbg[0] && i < 256; i++)
-            fprintf(stderr, "  round %llu entry %llu lane %llu addr/idx %llx\n", h_dbg[1 + 4 * i], h_dbg[2 + 4 * i],
-                    h_dbg[3 + 4 * i], h_dbg[4 + 4 * i]);
-    }
-#endif
     (void)hipFreeAsync(buf, st);
     JL_HIP(e);
     return JL_OK;
@@ -691,28 +650,6 @@ int run_general(const jlk::KParams &P, hipStream_t st) {
     const bool small = P.off && P.n < 4096 && P.mode != jlk::MODE_CRC;
     const bool want_gv4 = o.general_path == JL_PATH_GV4 || (o.general_path == JL_PATH_AUTO && !small);
     if (want_gv4 && gv4_eligible(P)) return run_gv4(P, st);
-#if JL_STUDY
-    if (o.general_path == 3 && !getenv("JL_STREAM_DEBUG")) {  // the r1 chunked kernel
-        JL_HIP(jlk::launch_general(ctx().d_img, P, grid_for(P.n), st));
-        return JL_OK;
-    }
-    if (const char *dbg = getenv("JL_STREAM_DEBUG")) {  // "lo:hi" valid load range (hex), debugging only
-        jlk::KParams Q = P;
-        Q.dbg_lo = strtoull(dbg, nullptr, 16);
-        const char *c = strchr(dbg, ':');
-        Q.dbg_hi = c ? strtoull(c + 1, nullptr, 16) : ~0ull;
-        unsigned long long *d_dbg = nullptr, h_dbg[1 + 4 * 256];
-        JL_HIP(hipMalloc((void **)&d_dbg, sizeof(h_dbg)));
-        JL_HIP(hipMemsetAsync(d_dbg, 0, sizeof(h_dbg), st));
-        Q.dbg = d_dbg;
-        JL_HIP(jlk::launch_stream(ctx().d_img, Q, nullptr, grid_for(P.n), o.stream_depth, st));
-        JL_HIP(hipMemcpyAsync(h_dbg, d_dbg, sizeof(h_dbg), hipMemcpyDeviceToHost, st));
-        JL_HIP(hipStreamSynchronize(st));
-        (void)hipFree(d_dbg);
-        fprintf(stderr, "JL_STREAM_DEBUG mode=%d n=%llu bad=%llu\n", P.mode, (unsigned long long)P.n, h_dbg[0]);
-        return JL_OK;
-    }
-#endif
     const int grid = grid_for(P.n);
     int rc = JL_OK;
     uint64_t *part = make_partition(P, (uint64_t)grid * 16, st, &rc);
@@ -744,7 +681,7 @@ int jl_set_option(int option, int64_t value) {
     Options &o = opt();
     switch (option) {
     case JL_OPT_GENERAL_PATH:
-        if (value < JL_PATH_AUTO || value > (JL_STUDY ? 3 : JL_PATH_GV4)) break;
+        if (value < JL_PATH_AUTO || value > JL_PATH_GV4) break;
         o.general_path = (int)value;
         return JL_OK;
     case JL_OPT_STREAM_DEPTH:
@@ -776,9 +713,6 @@ int jl_set_option(int option, int64_t value) {
         o.log_host_threshold = value;
         return JL_OK;
 #if JL_STUDY
-    case JL_OPT_FIXED_KERNEL:
-        o.fixed_kernel = (int)value;
-        return JL_OK;
     case JL_OPT_GV4_VARIANT:
         if (value < 0 || value > 9) break;
         o.gv4_variant = (int)value;
@@ -801,7 +735,6 @@ int64_t jl_get_option(int option) {
     case JL_OPT_STAGE_THREADS: return o.stage_threads;
     case JL_OPT_HOST_THRESHOLD: return o.host_threshold;
     case JL_OPT_LOG_HOST_THRESHOLD: return o.log_host_threshold;
-    case JL_OPT_FIXED_KERNEL: return o.fixed_kernel;
     case JL_OPT_GV4_VARIANT: return o.gv4_variant;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
     }
@@ -899,27 +832,10 @@ int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blo
     if (!d_data || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: null pointer");
     if (block_bytes > 0xffffffffull) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: block_bytes >= 4 GiB");
     hipStream_t st = pick(stream);
-    if (block_bytes == 4096 && ((uintptr_t)d_data & 15) == 0) {
-        const int chains = opt().fixed_kernel;
-        if (chains == 7) {  // the v4 product kernel (fixed_v4.hip): 8 lanes/block, 8-slot ring, 1024 threads
-            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[1], (const uint8_t *)d_data, n_blocks, flags, d_out,
-                                          grid_for(n_blocks), 8, 1, 3, st));
-            return JL_OK;
-        }
-#if JL_STUDY
-        // study kernels: 8 = v4 16 lanes/block; 10 = v4 16-slot ring without nt; 11, 12 = v4 (8 slots, 512
-        // threads), (16 slots, 512 threads); 13 = v4 16-slot ring; 2..6, 101..104 = the r1 kernels
-        if (chains == 8 || (chains >= 10 && chains <= 13)) {
-            const int lpb = chains == 8 ? 16 : 8;
-            const int shape = (chains == 11 || chains == 12) ? chains - 10 : 0;
-            JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[lpb == 8 ? 1 : 2], (const uint8_t *)d_data, n_blocks, flags,
-                                          d_out, grid_for(n_blocks), lpb, chains != 10, shape, st));
-            return JL_OK;
-        }
-        JL_HIP(jlk::launch_fixed4k(ctx().d_img, (const uint8_t *)d_data, ctx().d_zero, n_blocks, flags, d_out,
-                                   ctx().d_scratch, grid_for(n_blocks), 1, 1, chains, st));
+    if (block_bytes == 4096 && ((uintptr_t)d_data & 15) == 0) {  // the v4 kernel (fixed_v4.hip)
+        JL_HIP(jlk::launch_fixed4k_v4(ctx().d_img_v4[1], (const uint8_t *)d_data, n_blocks, flags, d_out,
+                                      grid_for(n_blocks), st));
         return JL_OK;
-#endif
     }
     jlk::KParams P = base_params(d_data, n_blocks, jlk::MODE_CRC);
     P.fixed_bytes = block_bytes;
@@ -1110,9 +1026,12 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
     const uint64_t n = first[n_tables];
     if (first[0] != 0) return fail(JL_ERR_INVALID, "jl_tables_verify: first[0] must be 0");
     if (n && (!off || !size || !status)) return fail(JL_ERR_INVALID, "jl_tables_verify: null pointer");
+    // every handle range inside [0, first[n_tables]) before any off[] / size[] access
+    for (uint64_t t = 0; t < n_tables; t++)
+        if (first[t + 1] < first[t] || first[t + 1] > n)
+            return fail(JL_ERR_INVALID, "jl_tables_verify: handle ranges not ascending");
     uint64_t touched = 0;
     for (uint64_t t = 0; t < n_tables; t++) {
-        if (first[t + 1] < first[t]) return fail(JL_ERR_INVALID, "jl_tables_verify: handle ranges not ascending");
         if (first[t + 1] > first[t] && !files[t]) return fail(JL_ERR_INVALID, "jl_tables_verify: null table");
         for (uint64_t i = first[t]; i < first[t + 1]; i++) {
             if (off[i] > file_bytes[t] || (uint64_t)size[i] + 5 > file_bytes[t] - off[i])
@@ -1322,9 +1241,11 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // With pools (>= 8 blocks per lc_dense workgroup) a workgroup leaves less than a pool
     // unused at the end, and less than its next block's events (<= kLDMaxEv) per refill:
     // refills <= events / (pool - kLDMaxEv) + grid
+    // A count-only call (no event array) stashes nothing: lc_dense skips the stores
+    // of a block that does not fit (stash_cap 0), and lc_build has no events to write.
     const uint64_t need = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
     const uint64_t grid = jlk::lc_dense_grid(ctx().cus);
-    const uint64_t pool = nb >= 8 * grid ? jlk::kLDPool : 0;
+    const uint64_t pool = need && nb >= 8 * grid ? jlk::kLDPool : 0;
     const uint64_t stash_cap =
         pool ? need + (need / (pool - jlk::kLDMaxEv) + grid) * jlk::kLDMaxEv + grid * pool : need;
     JL_HIP(c.ws_stash.ensure(std::max<uint64_t>(stash_cap, 1) * 8));
@@ -1434,9 +1355,13 @@ static int ws_order(Workspace &w, hipStream_t st) {
     if (w.async_pending && w.async_st != st) JL_HIP(hipStreamWaitEvent(st, w.async_done, 0));
     return JL_OK;
 }
+// A synchronous call does not always synchronise its stream (an empty log returns
+// before any launch, and ws_order only made its stream wait on the device), so the
+// pending asynchronous call is waited for on the host before it is forgotten: a
+// completed event costs one query.
 static int ws_after(Workspace &w, hipStream_t st, bool async, int rc) {
     if (!async || rc) {
-        if (rc && w.async_pending) (void)hipEventSynchronize(w.async_done);
+        if (w.async_pending) (void)hipEventSynchronize(w.async_done);
         w.async_pending = false;
         return rc;
     }

@@ -1,21 +1,11 @@
-// jlcrc_kernels.hip — CDNA4 (gfx950) kernels of the masked-CRC32C engine:
-// the log-writer copy kernel, the partition, fill and read-stream
-// helpers, and — in the study build only (make STUDY=1, -DJL_STUDY=1) — the
-// round-1 kernels the v4 and general-v4 paths superseded, kept for A/B:
-//
-// [study] One wave (64 lanes) owns one block at a time.  A block of n bytes is viewed
-// end-aligned as K = ceil(n/256) "steps" of 256 bytes (f = 256K - n virtual
-// zero bytes in front); in step k lane l owns the 4-byte word at virtual offset
-// 256k + 4l.  Every step is one coalesced 256-B wave load (global_load_dword)
-// and, per lane, one slicing-by-4 update through the gap tables G (4 LDS
-// lookups, bank-conflict-free by construction).  After K steps lane l is
-// re-aligned with z^-(4l) (8 nibble lookups), the lanes are XOR-reduced with
-// DPP, and the masked crc is stored by lane 0.  Algebra and LDS layout:
-// crc_math.hpp and DESIGN.md §3.
-//
-// Persistent grid: one 1024-thread workgroup per CU (LDS = 160 KiB table image),
-// 16 waves per CU; each wave walks its blocks with a one-chunk-ahead prefetch of
-// the next 16 steps so the HBM stream never waits on the LDS chain.
+// jlcrc_kernels.hip — CDNA4 (gfx950) helper kernels of the masked-CRC32C engine:
+// the log-writer payload copy, the stream kernel's byte-balanced partition, the
+// event rebase of chunked host log verification, and the fill and read-stream
+// kernels of the benchmark (synthetic inputs, the HBM read ceiling).  The CRC
+// kernels live in fixed_v4.hip (4 KiB blocks), general_v4.hip (offset/length
+// batches, log record chunks), stream_kernel.hip (small batches, trailers,
+// headers), log_chunks.hip and log_stream.hip (WAL verification).  The round-1
+// kernels those superseded live on the git branch study-superseded-kernels.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -23,499 +13,7 @@
 
 #include "engine_device.hpp"
 
-#ifndef JL_STUDY
-#define JL_STUDY 0
-#endif
-
 namespace jlk {
-
-#if JL_STUDY
-// ---------------------------------------------------------------------------
-// Fast path: n_blocks contiguous 4 KiB blocks (one 16-step chunk each, f = 0).
-// Ping-pong register buffers: the 16 loads of the wave's next block are issued
-// (past the end: the zero page) before the current block's chain runs and are
-// pinned there with a sched_barrier; the result store is issued by every lane
-// to the same address (no divergent branch), so the loop body is one basic
-// block and the waitcnt pass can leave the next block's loads in flight.
-// ---------------------------------------------------------------------------
-template <bool NT>
-__device__ __forceinline__ void load16(uint32_t w[16], const uint32_t *p) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) w[k] = NT ? __builtin_nontemporal_load(p + 64 * k) : p[64 * k];
-}
-
-__device__ __forceinline__ uint32_t chain16(uint32_t s, const uint32_t w[16], const uint32_t *lds, const GLanes &gl) {
-#pragma unroll
-    for (int k = 0; k < 16; k++) s = gstep(lds, s ^ w[k], gl);
-    return s;
-}
-
-// 16 coalesced dword loads of one 4 KiB block, issued as inline asm so that the
-// compiler cannot re-rotate them around the chain; the matching waits are
-// wait16() below.  base is wave-uniform (SGPR pair), voff = 4*lane.
-template <bool NT>
-__device__ __forceinline__ void asm_load16(uint32_t w[16], const void *base, uint32_t voff) {
-#define JL_LD(k, off)                                                                                    \
-    if (NT) asm volatile("global_load_dword %0, %1, %2 offset:" #off " nt" : "=v"(w[k]) : "v"(voff), "s"(base) : "memory"); \
-    else asm volatile("global_load_dword %0, %1, %2 offset:" #off : "=v"(w[k]) : "v"(voff), "s"(base) : "memory");
-    JL_LD(0, 0) JL_LD(1, 256) JL_LD(2, 512) JL_LD(3, 768) JL_LD(4, 1024) JL_LD(5, 1280) JL_LD(6, 1536)
-    JL_LD(7, 1792) JL_LD(8, 2048) JL_LD(9, 2304) JL_LD(10, 2560) JL_LD(11, 2816) JL_LD(12, 3072)
-    JL_LD(13, 3328) JL_LD(14, 3584) JL_LD(15, 3840)
-#undef JL_LD
-}
-
-// Chain over a block whose 16 loads were followed by the 16-load batches of D
-// later blocks (plus at most D stores): word k is complete once at most
-// 15-k + 16*D vector-memory operations are outstanding.
-// ABL (tuning ablations only, results wrong when != 0): 1 = VALU mix instead
-// of the LDS lookups, 2 = plain XOR of the words.
-template <int D, int ABL>
-__device__ __forceinline__ uint32_t chain16_waited(uint32_t s, uint32_t w[16], const uint32_t *lds, const GLanes &gl) {
-#define JL_STEP(k)                                                                    \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[k]) : "n"(15 - k + 16 * D));         \
-    if (ABL == 0) s = gstep(lds, s ^ w[k], gl);                                       \
-    else if (ABL == 1) { uint32_t x = s ^ w[k]; s = (x * 0x9E3779B1u) ^ (x >> 7); }  \
-    else s ^= w[k];
-    JL_STEP(0) JL_STEP(1) JL_STEP(2) JL_STEP(3) JL_STEP(4) JL_STEP(5) JL_STEP(6) JL_STEP(7)
-    JL_STEP(8) JL_STEP(9) JL_STEP(10) JL_STEP(11) JL_STEP(12) JL_STEP(13) JL_STEP(14) JL_STEP(15)
-#undef JL_STEP
-    return s;
-}
-
-// Block order and result stores.  A wave owns groups of 64 consecutive blocks
-// (group g = wave, wave + W, ...; W = waves in the grid) and walks them block
-// by block with a one-to-D-block-ahead prefetch.  Block j's crc goes to lane j
-// of one VGPR (a lane-select) and the group's 64 results leave as ONE coalesced
-// 256-B store: a 4-B store per block from many CUs/XCDs into shared lines cost
-// ~9% of the kernel (r1 ablation).
-struct GroupIter {
-    uint64_t n_blocks, waves, g, j;  // group, block-in-group
-    __device__ __forceinline__ uint64_t block() const { return g * 64u + j; }
-    __device__ __forceinline__ void advance() {
-        if (++j == 64u || block() >= n_blocks) { j = 0; g += waves; }
-    }
-};
-
-template <bool NT, int D, int ABL = 0>
-__global__ __launch_bounds__(1024) void crc_fixed4k_kernel(const uint4 *__restrict__ img,
-                                                           const uint8_t *__restrict__ data,
-                                                           const uint8_t *__restrict__ zero, uint64_t n_blocks,
-                                                           uint32_t flags, uint32_t *__restrict__ out) {
-    static_assert(D >= 1 && D <= 3, "vmcnt is 6 bits: at most 3 blocks ahead");
-    __shared__ uint32_t lds[kImageBytes / 4];
-    load_image(lds, img);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t voff = lane * 4u;
-    const uint32_t l4lo = (lane & 31u) << 2;
-    const GLanes gl(lane);
-    const uint32_t lc = 131072u | ((lane >> 5) << 14) | l4lo;
-    const uint32_t s_init = (lane == 0) ? 0xffffffffu : 0u;
-    const uint32_t do_mask = flags & 1u;
-    GroupIter cur;
-    cur.n_blocks = n_blocks;
-    cur.waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    cur.g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    cur.j = 0;
-    if (cur.block() >= n_blocks) return;
-    GroupIter pre = cur;  // prefetch cursor, D blocks ahead
-    uint32_t w[D + 1][16];
-#pragma unroll
-    for (int j = 0; j < D; j++) {
-        const uint64_t bj = pre.block();
-        asm_load16<NT>(w[j], bj < n_blocks ? data + bj * 4096u : zero, voff);
-        pre.advance();
-    }
-    uint32_t res = 0;
-    for (;;) {
-#pragma unroll
-        for (int j = 0; j <= D; j++) {
-            const uint64_t bp = pre.block();
-            asm_load16<NT>(w[(j + D) % (D + 1)], bp < n_blocks ? data + bp * 4096u : zero, voff);
-            pre.advance();
-            uint32_t crc;
-            if (ABL >= 3) crc = chain16_waited<D, 2>(s_init, w[j], lds, gl);
-            else crc = ~wave_xor(realign(lds, chain16_waited<D, ABL>(s_init, w[j], lds, gl), lc));
-            res = (lane == (uint32_t)cur.j) ? (do_mask ? mask_crc(crc) : crc) : res;
-            const uint64_t g0 = cur.g * 64u;
-            cur.advance();
-            if (cur.j == 0) {  // group complete: one coalesced store of up to 64 results
-                if (ABL != 4 && g0 + lane < n_blocks) out[g0 + lane] = res;
-                if (cur.block() >= n_blocks) goto done;
-            }
-        }
-    }
-done:
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the zero-page prefetches
-}
-
-// Two-chain variant: a wave runs two independent blocks' chains interleaved
-// (8 LDS lookups in flight per step instead of 4).  The 32 loads of a block
-// pair are issued interleaved (A0 B0 A1 B1 ...) and the next pair's 32 loads
-// are in flight while the current pair is consumed, so A_k is complete at
-// vmcnt(63-2k) and B_k at vmcnt(62-2k).  Results of a pair member past the end
-// of an odd group tail read the zero page and are never stored.
-template <bool NT>
-__device__ __forceinline__ void asm_load32x2(uint32_t a[16], uint32_t b[16], const void *pa, const void *pb,
-                                             uint32_t voff) {
-#define JL_LD2(k, off)                                                                                            \
-    if (NT) {                                                                                                     \
-        asm volatile("global_load_dword %0, %1, %2 offset:" #off " nt" : "=v"(a[k]) : "v"(voff), "s"(pa) : "memory"); \
-        asm volatile("global_load_dword %0, %1, %2 offset:" #off " nt" : "=v"(b[k]) : "v"(voff), "s"(pb) : "memory"); \
-    } else {                                                                                                      \
-        asm volatile("global_load_dword %0, %1, %2 offset:" #off : "=v"(a[k]) : "v"(voff), "s"(pa) : "memory");       \
-        asm volatile("global_load_dword %0, %1, %2 offset:" #off : "=v"(b[k]) : "v"(voff), "s"(pb) : "memory");       \
-    }
-    JL_LD2(0, 0) JL_LD2(1, 256) JL_LD2(2, 512) JL_LD2(3, 768) JL_LD2(4, 1024) JL_LD2(5, 1280) JL_LD2(6, 1536)
-    JL_LD2(7, 1792) JL_LD2(8, 2048) JL_LD2(9, 2304) JL_LD2(10, 2560) JL_LD2(11, 2816) JL_LD2(12, 3072)
-    JL_LD2(13, 3328) JL_LD2(14, 3584) JL_LD2(15, 3840)
-#undef JL_LD2
-}
-
-__device__ __forceinline__ void chain_pair(uint32_t &sa, uint32_t &sb, uint32_t a[16], uint32_t b[16],
-                                           const uint32_t *lds, const GLanes &gl) {
-#define JL_STEP2(k)                                                               \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a[k]) : "n"(63 - 2 * k));           \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(b[k]) : "n"(62 - 2 * k));           \
-    {                                                                             \
-        uint32_t xa = sa ^ a[k], xb = sb ^ b[k];                                  \
-        sa = gstep(lds, xa, gl);                                                  \
-        sb = gstep(lds, xb, gl);                                                  \
-    }
-    JL_STEP2(0) JL_STEP2(1) JL_STEP2(2) JL_STEP2(3) JL_STEP2(4) JL_STEP2(5) JL_STEP2(6) JL_STEP2(7)
-    JL_STEP2(8) JL_STEP2(9) JL_STEP2(10) JL_STEP2(11) JL_STEP2(12) JL_STEP2(13) JL_STEP2(14) JL_STEP2(15)
-#undef JL_STEP2
-}
-
-// chain_pair with the data XOR folded into the previous step's xor3: on entry
-// the states are the raw chain states (s_init); a[k]/b[k] wait as in chain_pair.
-__device__ __forceinline__ void chain_pair_x3(uint32_t &sa, uint32_t &sb, uint32_t a[16], uint32_t b[16],
-                                              const uint32_t *lds, const GLanes &gl) {
-    asm volatile("s_waitcnt vmcnt(63)" : "+v"(a[0]));
-    asm volatile("s_waitcnt vmcnt(62)" : "+v"(b[0]));
-    uint32_t xa = sa ^ a[0], xb = sb ^ b[0];
-#define JL_STEP3(k)                                                               \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(a[k]) : "n"(63 - 2 * k));           \
-    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(b[k]) : "n"(62 - 2 * k));           \
-    xa = gstep_x3(lds, xa, gl, a[k]);                                             \
-    xb = gstep_x3(lds, xb, gl, b[k]);
-    JL_STEP3(1) JL_STEP3(2) JL_STEP3(3) JL_STEP3(4) JL_STEP3(5) JL_STEP3(6) JL_STEP3(7) JL_STEP3(8)
-    JL_STEP3(9) JL_STEP3(10) JL_STEP3(11) JL_STEP3(12) JL_STEP3(13) JL_STEP3(14) JL_STEP3(15)
-#undef JL_STEP3
-    sa = gstep_x3(lds, xa, gl, 0u);
-    sb = gstep_x3(lds, xb, gl, 0u);
-}
-
-template <bool NT, bool X3 = false, bool PRIO = false>
-__global__ __launch_bounds__(1024) void crc_fixed4k_x2_kernel(const uint4 *__restrict__ img,
-                                                              const uint8_t *__restrict__ data,
-                                                              const uint8_t *__restrict__ zero, uint64_t n_blocks,
-                                                              uint32_t flags, uint32_t *__restrict__ out) {
-    __shared__ uint32_t lds[kImageBytes / 4];
-    load_image(lds, img);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t voff = lane * 4u;
-    const uint32_t l4lo = (lane & 31u) << 2;
-    const GLanes gl(lane);
-    const uint32_t lc = 131072u | ((lane >> 5) << 14) | l4lo;
-    const uint32_t s_init = (lane == 0) ? 0xffffffffu : 0u;
-    const uint32_t do_mask = flags & 1u;
-    // pairs (2i, 2i+1) of 64-block groups; group g = wave, wave + W, ...
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint64_t g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    if (g * 64u >= n_blocks) return;
-    uint64_t pg = g, pj = 0;  // prefetch cursor (one pair ahead)
-    auto src = [&](uint64_t blk) -> const uint8_t * { return blk < n_blocks ? data + blk * 4096u : zero; };
-    auto adv = [&](uint64_t &gg, uint64_t &jj) {
-        jj += 2;
-        if (jj == 64u || gg * 64u + jj >= n_blocks) { jj = 0; gg += waves; }
-    };
-    uint32_t a0[16], b0[16], a1[16], b1[16];
-    asm_load32x2<NT>(a0, b0, src(pg * 64u + pj), src(pg * 64u + pj + 1), voff);
-    adv(pg, pj);
-    uint64_t j = 0;
-    uint32_t res = 0;
-    for (;;) {
-#define JL_PAIR(CA, CB, NA, NB)                                                                          \
-    {                                                                                                    \
-        if (PRIO) __builtin_amdgcn_s_setprio(3);                                                          \
-        asm_load32x2<NT>(NA, NB, src(pg * 64u + pj), src(pg * 64u + pj + 1), voff);                      \
-        if (PRIO) __builtin_amdgcn_s_setprio(0);                                                          \
-        adv(pg, pj);                                                                                     \
-        uint32_t sa = s_init, sb = s_init;                                                               \
-        if (X3) chain_pair_x3(sa, sb, CA, CB, lds, gl);                                                  \
-        else chain_pair(sa, sb, CA, CB, lds, gl);                                                        \
-        uint32_t ca = ~wave_xor(realign(lds, sa, lc)), cb = ~wave_xor(realign(lds, sb, lc));             \
-        if (do_mask) { ca = mask_crc(ca); cb = mask_crc(cb); }                                           \
-        res = (lane == (uint32_t)j) ? ca : res;                                                          \
-        res = (lane == (uint32_t)j + 1) ? cb : res;                                                      \
-        const uint64_t g0 = g * 64u;                                                                     \
-        j += 2;                                                                                          \
-        if (j == 64u || g0 + j >= n_blocks) {                                                            \
-            if (g0 + lane < n_blocks) out[g0 + lane] = res;                                              \
-            j = 0;                                                                                       \
-            g += waves;                                                                                  \
-            if (g * 64u >= n_blocks) break;                                                              \
-        }                                                                                                \
-    }
-        JL_PAIR(a0, b0, a1, b1)
-        JL_PAIR(a1, b1, a0, b0)
-#undef JL_PAIR
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---------------------------------------------------------------------------
-// General path: arbitrary lengths / alignment, per-block init & suffix and the
-// epilogue modes of the caller shims (plain crc, table trailer, table verify,
-// log header, log verify).
-//
-// A block of n bytes is end-aligned to whole 16-step chunks: f = 4096*chunks - n
-// virtual zero bytes in front.  Zero words leave a zero chain state unchanged,
-// so chunk 0 enters its unrolled chain at the first step that holds real data
-// (k0 = f >> 8, a Duff's-device switch) and the other chunks run all 16 steps.
-// The initial state z^-r(~init) (r = f & 3) seeds lane l0 = (f >> 2) & 63, the
-// lane whose step-k0 word holds real byte 0; when that word straddles the block
-// start its bytes come from two ALIGNED dwords (an aligned dword that overlaps
-// the block never leaves its pages) combined with v_alignbyte.
-//
-// Every work item (one chunk) issues a fixed batch of 19 loads as inline asm:
-// E0, E1 (straddle dwords), E2 (stored crc for the verify modes), w0..w15; loads
-// nobody needs read the zero page.  The next item's batch is issued before the
-// current chain runs, so word k is complete at vmcnt(34-k) and E0..E2 at
-// vmcnt(35).  Results of 64 consecutive blocks are collected in one VGPR and
-// leave as one coalesced store (see GroupIter).
-// ---------------------------------------------------------------------------
-struct BlockDesc {
-    const uint8_t *ptr;  // first byte
-    uint32_t n;          // bytes covered by the crc
-    uint32_t init;       // extend() initial crc
-    uint32_t suffix;     // 0x100 | byte, or 0
-    uint32_t chunks;     // ceil(n/4096) (0 for n == 0)
-    uint32_t f;          // 4096*chunks - n
-};
-
-// Descriptor arrays as restrict kernel arguments: with noalias against the
-// outputs the compiler reads them with scalar loads (s_load), which do not
-// touch vmcnt and so never drain the hand-counted load pipeline.
-struct DescArgs {
-    const uint64_t *__restrict__ off;
-    const uint32_t *__restrict__ len;
-    const uint32_t *__restrict__ init;
-    const uint8_t *__restrict__ suffix;
-    const uint8_t *__restrict__ type;
-    const uint32_t *__restrict__ aux;
-};
-
-__device__ __forceinline__ BlockDesc get_desc(const KParams &P, const DescArgs &A, uint64_t i) {
-    BlockDesc d;
-    uint64_t off;
-    uint32_t n;
-    if (A.off) {
-        off = A.off[i];
-        n = A.len[i] + P.len_add;
-    } else {
-        off = i * P.fixed_bytes;
-        n = (uint32_t)P.fixed_bytes;
-    }
-    d.ptr = P.base + off;
-    d.n = n;
-    uint32_t init = 0;
-    if (A.init) init = A.init[i];
-    if (P.mode == MODE_LOG_HEADER) init = saux(A.aux, 512 + sbyte(A.type, i) % 5u);
-    d.init = init;
-    uint32_t sfx = 0;
-    if (P.mode == MODE_TRAILER) sfx = 0x100u | (A.type ? sbyte(A.type, i) : 0u);
-    else if (A.suffix) sfx = 0x100u | sbyte(A.suffix, i);
-    d.suffix = sfx;
-    d.chunks = (uint32_t)(((uint64_t)n + 4095u) >> 12);
-    d.f = (d.chunks << 12) - n;
-    return d;
-}
-
-struct Batch {
-    uint32_t e0, e1, e2;
-    uint32_t w[16];
-};
-
-__device__ __forceinline__ void asm_ld(uint32_t &dst, const void *addr) {
-    asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(addr) : "memory");
-}
-
-// Issues the 19 loads of chunk `chunk` of block d (valid == false: zero page only).
-__device__ __forceinline__ void issue_batch(Batch &B, const KParams &P, const BlockDesc &d, bool valid,
-                                            uint32_t chunk, uint32_t lane) {
-    const uint8_t *zp = P.zero + 4 * lane;
-    const bool first = valid && chunk == 0;
-    const uint32_t l0 = (d.f >> 2) & 63u;
-    const bool strad = first && (d.f & 3u) && lane == l0;
-    const uintptr_t al = (uintptr_t)d.ptr & ~(uintptr_t)3;
-    const uintptr_t al_last = ((uintptr_t)d.ptr + d.n - 1) & ~(uintptr_t)3;
-    asm_ld(B.e0, strad ? (const void *)al : (const void *)zp);
-    asm_ld(B.e1, strad ? (const void *)(al + 4 <= al_last ? al + 4 : al_last) : (const void *)zp);
-    const bool last = valid && chunk + 1 == d.chunks;
-    const uint8_t *ea = zp;
-    if (last && P.mode == MODE_TABLE_VERIFY) ea = d.ptr + d.n;  // trailer crc after block || type
-    if (last && P.mode == MODE_LOG_VERIFY) ea = d.ptr - 6;      // header crc before type || payload
-    asm_ld(B.e2, ea);
-    const int64_t base_p = (int64_t)chunk * 4096 + 4 * (int64_t)lane - (int64_t)d.f;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int64_t p = base_p + 256 * k;
-        asm_ld(B.w[k], (valid && p >= 0) ? (const void *)(d.ptr + p) : (const void *)zp);
-    }
-}
-
-// Chain over one chunk entering at step k0 (0 for every chunk but the first).
-__device__ __forceinline__ uint32_t chain_from(uint32_t s, Batch &B, uint32_t k0, const uint32_t *lds,
-                                               const GLanes &gl) {
-#define JL_GS(k)                                                              \
-    case k:                                                                   \
-        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(B.w[k]) : "n"(34 - k));     \
-        s = gstep(lds, s ^ B.w[k], gl);                                       \
-        [[fallthrough]];
-    switch (k0) {
-        JL_GS(0) JL_GS(1) JL_GS(2) JL_GS(3) JL_GS(4) JL_GS(5) JL_GS(6) JL_GS(7)
-        JL_GS(8) JL_GS(9) JL_GS(10) JL_GS(11) JL_GS(12) JL_GS(13) JL_GS(14) JL_GS(15)
-    default:
-        break;
-    }
-#undef JL_GS
-    return s;
-}
-
-// Per-block epilogue.  MODE_CRC / verify results go to lane j of `res` (the
-// caller stores the group); trailers and log headers are written directly.
-__device__ __forceinline__ void epilogue(const KParams &P, const DescArgs &A, uint64_t i, const BlockDesc &d,
-                                         uint32_t crc, uint32_t stored, uint32_t lane, uint32_t j, uint32_t &res) {
-    const uint32_t m = mask_crc(crc);
-    uint32_t r = 0;
-    switch (P.mode) {
-    case MODE_CRC:
-        r = (P.flags & 1u) ? m : crc;
-        break;
-    case MODE_TABLE_VERIFY:
-        r = (stored == m) ? 1u : 0u;
-        break;
-    case MODE_LOG_VERIFY:  // n == 0: not an OK event (nothing to verify)
-        r = (d.n == 0 || stored == m) ? 1u : 0u;
-        break;
-    case MODE_TRAILER:
-        if (lane < 5) P.out8[5 * i + lane] = (lane == 0) ? (uint8_t)(d.suffix & 0xffu) : (uint8_t)(m >> (8 * (lane - 1)));
-        break;
-    case MODE_LOG_HEADER:
-        if (lane < 7) {
-            uint8_t *hdr = P.out8 + 7 * i;
-            if (P.hdr_off) {
-                const uint64_t *h = (const uint64_t *)(uintptr_t)uni64((uint64_t)(uintptr_t)(P.hdr_off + i));
-                hdr = P.out8 + (((uint64_t)sload((const uint32_t *)h + 1) << 32) | sload(h));
-            }
-            uint8_t b;
-            if (lane < 4) b = (uint8_t)(m >> (8 * lane));
-            else if (lane == 4) b = (uint8_t)(d.n & 0xffu);
-            else if (lane == 5) b = (uint8_t)((d.n >> 8) & 0xffu);
-            else b = (uint8_t)sbyte(A.type, i);
-            hdr[lane] = b;
-        }
-        break;
-    default:
-        break;
-    }
-    res = (lane == j) ? r : res;
-}
-
-struct GenCursor {
-    uint64_t g, j;     // group of 64 blocks, block in group
-    uint32_t chunk;    // chunk in block
-    BlockDesc d;
-    __device__ __forceinline__ uint64_t blk() const { return g * 64u + j; }
-};
-
-__device__ __forceinline__ void gen_advance(GenCursor &c, const KParams &P, const DescArgs &A, uint64_t waves) {
-    if (c.chunk + 1 < c.d.chunks) {
-        c.chunk++;
-        return;
-    }
-    c.chunk = 0;
-    if (++c.j == 64u || c.blk() >= P.n) {
-        c.j = 0;
-        c.g += waves;
-    }
-    if (c.blk() < P.n) c.d = get_desc(P, A, c.blk());
-}
-
-__global__ __launch_bounds__(1024) void crc_general_kernel(const uint4 *__restrict__ img, KParams P,
-                                                           const uint64_t *__restrict__ d_off,
-                                                           const uint32_t *__restrict__ d_len,
-                                                           const uint32_t *__restrict__ d_init,
-                                                           const uint8_t *__restrict__ d_suffix,
-                                                           const uint8_t *__restrict__ d_type,
-                                                           const uint32_t *__restrict__ d_aux) {
-    const DescArgs A{d_off, d_len, d_init, d_suffix, d_type, d_aux};
-    __shared__ uint32_t lds[kImageBytes / 4];
-    load_image(lds, img);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t l4lo = (lane & 31u) << 2;
-    const GLanes gl(lane);
-    const uint32_t lc = 131072u | ((lane >> 5) << 14) | l4lo;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    GenCursor cur;
-    cur.g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-    cur.j = 0;
-    cur.chunk = 0;
-    if (cur.blk() >= P.n) return;
-    cur.d = get_desc(P, A, cur.blk());
-    GenCursor nxt = cur;
-    Batch ba, bb;
-    issue_batch(ba, P, cur.d, cur.d.chunks != 0, 0, lane);
-    uint32_t s = 0, res = 0;
-    const bool group_out = P.mode == MODE_CRC || P.mode == MODE_TABLE_VERIFY || P.mode == MODE_LOG_VERIFY;
-    for (;;) {
-#define JL_ITEM(CB, NB)                                                                                   \
-    {                                                                                                     \
-        gen_advance(nxt, P, A, waves);                                                                    \
-        const bool nvalid = nxt.blk() < P.n && nxt.d.chunks != 0;                                        \
-        issue_batch(NB, P, nxt.d, nvalid, nxt.chunk, lane);                                               \
-        const BlockDesc &d = cur.d;                                                                       \
-        asm volatile("s_waitcnt vmcnt(35)" : "+v"(CB.e0), "+v"(CB.e1), "+v"(CB.e2));                     \
-        if (d.chunks) {                                                                                   \
-            uint32_t k0 = 0;                                                                              \
-            if (cur.chunk == 0) {                                                                         \
-                /* seed: z^-r(~init) at lane l0, XORed with the straddling bytes */                       \
-                uint32_t s0 = uni(~d.init);                                                               \
-                const uint32_t r = d.f & 3u, l0 = (d.f >> 2) & 63u;                                       \
-                for (uint32_t q = 0; q < r; q++) {                                                        \
-                    const uint32_t top = saux(A.aux, 256 + (s0 >> 24));                                   \
-                    s0 = uni(((s0 ^ saux(A.aux, top)) << 8) | top);                                       \
-                }                                                                                         \
-                const uint32_t m = (uint32_t)((uintptr_t)d.ptr & 3u);                                     \
-                const uint32_t wst = r ? (__builtin_amdgcn_alignbyte(CB.e1, CB.e0, m) << (8 * r)) : 0u;  \
-                s = (lane == l0) ? (s0 ^ wst) : 0u;                                                       \
-                k0 = (d.f >> 8) & 15u;                                                                    \
-            }                                                                                             \
-            s = chain_from(s, CB, k0, lds, gl);                                                           \
-        }                                                                                                 \
-        if (cur.chunk + 1 >= d.chunks) {                                                                  \
-            uint32_t t = d.chunks ? wave_xor(realign(lds, s, lc)) : ~d.init;                              \
-            if (d.suffix) t = (t >> 8) ^ saux(A.aux, (t ^ d.suffix) & 0xffu);                            \
-            const uint32_t stored = (uint32_t)__builtin_amdgcn_readfirstlane((int)CB.e2);                 \
-            epilogue(P, A, cur.blk(), d, ~t, stored, lane, (uint32_t)cur.j, res);                         \
-            const uint64_t g0 = cur.g * 64u;                                                              \
-            if (group_out && (cur.j == 63u || cur.blk() + 1 >= P.n) && g0 + lane < P.n) {                 \
-                if (P.mode == MODE_CRC) P.out32[g0 + lane] = res;                                         \
-                else P.out8[g0 + lane] = (uint8_t)res;                                                    \
-            }                                                                                             \
-        }                                                                                                 \
-        cur = nxt;                                                                                        \
-        if (cur.blk() >= P.n) break;                                                                      \
-    }
-        JL_ITEM(ba, bb)
-        JL_ITEM(bb, ba)
-#undef JL_ITEM
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-#endif  // JL_STUDY
 
 // Payload copies of a batched LogWriter (jl_log_emit_dev): one workgroup per
 // fragment (grid-stride), byte-granular (arbitrary alignment on both sides);
@@ -610,65 +108,6 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const uint8_t *__restr
 
 // ----------------------------------------------------------------- launchers
 namespace jlk {
-
-#if JL_STUDY
-hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
-                          uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
-                          hipStream_t st) {
-    if (chains == 3) {  // two chains + bitop3 XOR folding (default)
-        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img,
-                           data, zero, n_blocks, flags, out);
-        return hipGetLastError();
-    }
-    if (chains == 4) {  // A/B: + s_setprio 3 around the load issue
-        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true, true>), dim3(grid), dim3(1024), 0, st,
-                           (const uint4 *)img, data, zero, n_blocks, flags, out);
-        return hipGetLastError();
-    }
-    if (chains == 5 || chains == 6) {  // A/B: 8 / 12 waves per CU
-        hipLaunchKernelGGL((crc_fixed4k_x2_kernel<true, true>), dim3(grid), dim3(chains == 5 ? 512 : 768), 0, st,
-                           (const uint4 *)img, data, zero, n_blocks, flags, out);
-        return hipGetLastError();
-    }
-    if (chains == 2) {
-        if (nt)
-            hipLaunchKernelGGL(crc_fixed4k_x2_kernel<true>, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data,
-                               zero, n_blocks, flags, out);
-        else
-            hipLaunchKernelGGL(crc_fixed4k_x2_kernel<false>, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data,
-                               zero, n_blocks, flags, out);
-        return hipGetLastError();
-    }
-#define JL_L(NTV, DV)                                                                                          \
-    hipLaunchKernelGGL((crc_fixed4k_kernel<NTV, DV>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, data, zero, \
-                       n_blocks, flags, out)
-    if (chains > 100) {  // ablations (tuning only; results are wrong)
-#define JL_A(A) hipLaunchKernelGGL((crc_fixed4k_kernel<true, 1, A>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, \
-                                   data, zero, n_blocks, flags, out)
-        if (chains == 101) JL_A(1);
-        else if (chains == 102) JL_A(2);
-        else if (chains == 103) JL_A(3);
-        else JL_A(4);
-#undef JL_A
-        return hipGetLastError();
-    }
-    // one block ahead only: the deeper r1 variants (D = 2, 3) counted the group's
-    // result store as a younger vmcnt operation, which the ring checker
-    // (tools/asm_ring_check.py) cannot prove safe; they were never faster
-    (void)depth;
-    if (nt) JL_L(true, 1);
-    else JL_L(false, 1);
-#undef JL_L
-    return hipGetLastError();
-}
-
-hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st) {
-    hipLaunchKernelGGL(crc_general_kernel, dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P, P.off, P.len, P.init,
-                       P.suffix, P.type, P.aux);
-    return hipGetLastError();
-}
-
-#endif  // JL_STUDY
 
 hipError_t launch_stream(const void *img, const KParams &P, const uint64_t *part, int grid, int depth, hipStream_t st) {
     switch (P.mode) {

@@ -188,16 +188,9 @@ __host__ __device__ inline bool block_in_range(const KParams &P, uint64_t off, u
     return off <= P.base_bytes && need <= P.base_bytes - off;
 }
 
-// study build only (JL_STUDY): the round-1 4 KiB kernels and the chunked general kernel
-hipError_t launch_fixed4k(const void *img, const uint8_t *data, const uint8_t *zero, uint64_t n_blocks,
-                          uint32_t flags, uint32_t *out, uint32_t *scratch, int grid, int nt, int depth, int chains,
-                          hipStream_t st);
-// v4 fast path (fixed_v4.hip): lpb = lanes per block (8, 16); img = the v4 image for that lpb;
-// the product launches lpb 8, nt, shape 3 (8 ring slots, 1024 threads); the other
-// shapes exist in the study build only
+// v4 fast path (fixed_v4.hip): 8 lanes per block, 8 ring slots, 1024 threads; img = the 8-lane v4 image
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
-                             int grid, int lpb, int nt, int shape, hipStream_t st);
-hipError_t launch_general(const void *img, const KParams &P, int grid, hipStream_t st);
+                             int grid, hipStream_t st);
 // general v4 main kernel, one specialisation per mode (general_v4.hip -DJL_MODE=k; modes 0, 1, 5)
 template <int MODE>
 hipError_t launch_gv4_m(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st);

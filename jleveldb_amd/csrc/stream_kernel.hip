@@ -406,13 +406,6 @@ drain:
 template <>
 hipError_t launch_stream_m<JL_MODE>(const void *img, const KParams &P, const uint64_t *part, int grid, int depth,
                                     hipStream_t st) {
-#if JL_STUDY
-    if (P.dbg) {  // address-check build (JL_STREAM_DEBUG)
-        hipLaunchKernelGGL((crc_stream_kernel<JL_MODE, 32, true>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P,
-                           part);
-        return hipGetLastError();
-    }
-#endif
     if (depth <= 16)
         hipLaunchKernelGGL((crc_stream_kernel<JL_MODE, 16>), dim3(grid), dim3(1024), 0, st, (const uint4 *)img, P, part);
     else if (depth <= 32)

@@ -156,6 +156,21 @@ def job_wall_time(local_seconds: float, device=None) -> float:
     return float(t.item())
 
 
+def per_rank(value: float, device=None) -> list[float]:
+    """Every rank's value of one float, in rank order (one all_gather; [value]
+    without a process group): bench.py reports the per-rank kernel times beside
+    their MAX so a slow rank is visible."""
+    import torch
+    import torch.distributed as dist
+
+    if _pg_world() == 1:
+        return [float(value)]
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_coll_device(device))
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def total_mismatches(local_count: int, device=None) -> int:
     """Verify modes: SUM over ranks of the blocks / records that failed their CRC
     (one all_reduce of one integer; a no-op without a process group)."""

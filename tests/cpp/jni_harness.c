@@ -449,9 +449,171 @@ static void device_paths(const uint8_t *sst, size_t sst_n, const uint8_t *log, s
     free(want);
 }
 
+/* ------------------------------------------------------------------ dump mode
+ * What the Java side of Crc32CShims sees, written to a file for
+ * tests/test_jni.py to compare with the oracle (not with the C-ABI):
+ *   table:  Crc32CShims.verifyTable — tableBlockHandles from 64 entries with
+ *           grow-and-retry, then tableVerify over the exact handles
+ *           (TableFormat.java:211-212 for every block of Table.open)
+ *   tables: a compaction's inputs (VersionSet.java:820-823) — each table's
+ *           handles, then one tablesVerify call over all of them
+ *   log:    Crc32CShims.verifyLog — its capacity guess, logVerify, one grow to
+ *           the reported count, and its decoding of the 16-B little-endian
+ *           events (Crc32CShims.java:153-158), restated here byte by byte
+ *           (LogReader.java:297-383 for every physical record) */
+static FILE *g_out;
+static void put(const void *p, size_t n) { CHECK(fwrite(p, 1, n, g_out) == n, "short write"); }
+
+/* Crc32CShims.verifyTable's handle walk: the count, arrays of exactly that length */
+static jlong shim_handles(struct _jobject *buf, struct _jobject **o, struct _jobject **s, struct _jobject **k) {
+    *o = array(K_LONG, 64), *s = array(K_INT, 64), *k = array(K_BYTE, 64);
+    jlong n = JFN(tableBlockHandles)(env, NULL, buf, *o, *s, *k);
+    if (n > 64) {
+        release(*o), release(*s), release(*k);
+        *o = array(K_LONG, (jsize)n), *s = array(K_INT, (jsize)n), *k = array(K_BYTE, (jsize)n);
+        n = JFN(tableBlockHandles)(env, NULL, buf, *o, *s, *k);
+    }
+    CHECK(n >= 0 && g_exc[0] == 0, "tableBlockHandles: %lld %s", (long long)n, JFN(lastError)(env, NULL)->text);
+    if (n >= 0) (*o)->len = (*s)->len = (*k)->len = (jsize)n; /* Arrays.copyOf(.., n) */
+    return n;
+}
+
+static int dump_table(const char *path) {
+    size_t fn = 0;
+    uint8_t *f = read_file(path, &fn);
+    if (!f) return 2;
+    struct _jobject *buf = direct(f, (jlong)fn), *o, *s, *k;
+    const jlong n = shim_handles(buf, &o, &s, &k);
+    struct _jobject *ok = array(K_BYTE, (jsize)(n > 0 ? n : 0));
+    const jint rc = n >= 0 ? JFN(tableVerify)(env, NULL, buf, o, s, ok) : -1;
+    CHECK(rc == JL_OK && g_exc[0] == 0, "tableVerify: %d", rc);
+    const uint64_t nn = n > 0 ? (uint64_t)n : 0;
+    put(&nn, 8);
+    put(o->data, nn * 8), put(s->data, nn * 4), put(k->data, nn), put(ok->data, nn);
+    release(o), release(s), release(k), release(ok), release(buf);
+    free(f);
+    return 0;
+}
+
+static int dump_tables(int nt, char **paths) {
+    uint8_t **f = calloc((size_t)nt, sizeof *f);
+    struct _jobject **b = calloc((size_t)nt, sizeof *b);
+    struct _jobject *fa = array(K_OBJARRAY, nt), *fi = array(K_LONG, nt + 1);
+    fa->data = realloc(fa->data, (size_t)nt * sizeof(jobject));
+    jlong total = 0;
+    struct _jobject **ho = calloc((size_t)nt, sizeof *ho), **hs = calloc((size_t)nt, sizeof *hs);
+    for (int t = 0; t < nt; t++) {
+        size_t fn = 0;
+        if (!(f[t] = read_file(paths[t], &fn))) return 2;
+        b[t] = direct(f[t], (jlong)fn);
+        ((jobject *)fa->data)[t] = b[t];
+        struct _jobject *k;
+        ((jlong *)fi->data)[t] = total;
+        const jlong n = shim_handles(b[t], &ho[t], &hs[t], &k);
+        release(k);
+        total += n > 0 ? n : 0;
+    }
+    ((jlong *)fi->data)[nt] = total;
+    struct _jobject *o = array(K_LONG, (jsize)total), *s = array(K_INT, (jsize)total), *st = array(K_BYTE, (jsize)total);
+    for (int t = 0; t < nt; t++) {
+        const jlong a = ((jlong *)fi->data)[t], m = ((jlong *)fi->data)[t + 1] - a;
+        memcpy((jlong *)o->data + a, ho[t]->data, (size_t)m * 8);
+        memcpy((jint *)s->data + a, hs[t]->data, (size_t)m * 4);
+        release(ho[t]), release(hs[t]);
+    }
+    const jint rc = JFN(tablesVerify)(env, NULL, fa, fi, o, s, st);
+    CHECK(rc == JL_OK && g_exc[0] == 0 && g_local_refs == 0, "tablesVerify: %d", rc);
+    const uint64_t T = (uint64_t)nt;
+    put(&T, 8);
+    put(fi->data, (T + 1) * 8);
+    put(o->data, (size_t)total * 8), put(s->data, (size_t)total * 4), put(st->data, (size_t)total);
+    for (int t = 0; t < nt; t++) release(b[t]), free(f[t]);
+    release(fa), release(fi), release(o), release(s), release(st);
+    free(f), free(b), free(ho), free(hs);
+    return 0;
+}
+
+/* ByteBuffer.order(LITTLE_ENDIAN).getLong / getInt / get of the shim's decode */
+static uint64_t le(const uint8_t *p, int n) {
+    uint64_t v = 0;
+    for (int i = n - 1; i >= 0; i--) v = v << 8 | p[i];
+    return v;
+}
+
+static int dump_log(const char *path, int checksum) {
+    size_t ln = 0;
+    uint8_t *l = read_file(path, &ln);
+    if (!l) return 2;
+    struct _jobject *lb = direct(l, (jlong)ln);
+    const int64_t size = (int64_t)ln, imax = 2147483647;
+    int64_t cap = size / 7 + 2;
+    if (cap > (imax - 15) / 16) cap = (imax - 15) / 16;
+    if (cap > (size / 512 > 1024 ? size / 512 : 1024)) cap = size / 512 > 1024 ? size / 512 : 1024;
+    uint8_t *eb = calloc((size_t)cap, 16);
+    struct _jobject *ev = direct(eb, 16 * cap);
+    jlong n = JFN(logVerify)(env, NULL, lb, (jboolean)checksum, ev);
+    const int grew = n > cap;
+    if (n > cap) { /* the count came back: grow once */
+        release(ev);
+        free(eb);
+        cap = n;
+        eb = calloc((size_t)cap, 16);
+        ev = direct(eb, 16 * cap);
+        n = JFN(logVerify)(env, NULL, lb, (jboolean)checksum, ev);
+    }
+    CHECK(n >= 0 && n <= cap && g_exc[0] == 0, "logVerify: %lld", (long long)n);
+    const uint64_t nn = n > 0 ? (uint64_t)n : 0;
+    put(&nn, 8);
+    const uint64_t g = (uint64_t)grew;
+    put(&g, 8);
+    for (uint64_t i = 0; i < nn; i++) {
+        const uint8_t *e = eb + 16 * i;
+        /* new LogEvent(getLong(b), getInt(b + 8), get(b + 12) & 0xff, get(b + 13) & 0xff) */
+        const uint64_t offset = le(e, 8);
+        const uint32_t length = (uint32_t)le(e + 8, 4);
+        const uint8_t type = e[12], kind = e[13];
+        const jl_log_event back = {offset, length, type, kind, 0};
+        CHECK(memcmp(&back, e, 14) == 0, "event %llu: the shim's decode does not round-trip", (unsigned long long)i);
+        uint8_t rec[16] = {0};
+        memcpy(rec, &offset, 8), memcpy(rec + 8, &length, 4), rec[12] = type, rec[13] = kind;
+        put(rec, 16);
+    }
+    release(ev), release(lb);
+    free(eb);
+    free(l);
+    return 0;
+}
+
+static int dump(int argc, char **argv) {
+    /* dump[-default] <out> table <sst> | tables <sst>... | log <log> <checksum 0|1> */
+    if (argc < 5) return 2;
+    jint r = JFN(init)(env, NULL, 0);
+    CHECK(r == JL_OK, "init returned %d", r);
+    if (strcmp(argv[1], "dump") == 0) { /* every call on the device (the shim's thresholds at 0) */
+        CHECK(JFN(setOption)(env, NULL, JL_OPT_HOST_THRESHOLD, 0) == JL_OK, "threshold 0");
+        CHECK(JFN(setOption)(env, NULL, JL_OPT_LOG_HOST_THRESHOLD, 0) == JL_OK, "log threshold 0");
+    }
+    if (!(g_out = fopen(argv[2], "wb"))) return 2;
+    int rc = 2;
+    if (strcmp(argv[3], "table") == 0) rc = dump_table(argv[4]);
+    else if (strcmp(argv[3], "tables") == 0) rc = dump_tables(argc - 4, argv + 4);
+    else if (strcmp(argv[3], "log") == 0 && argc > 5) rc = dump_log(argv[4], atoi(argv[5]));
+    fclose(g_out);
+    CHECK(g_critical == 0 && g_exc[0] == 0, "left a critical region open or an exception pending");
+    if (rc) return rc;
+    if (g_fail) {
+        fprintf(stderr, "FAILED %d of %d\n", g_fail, g_checks);
+        return 1;
+    }
+    printf("OK %d\n", g_checks);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strncmp(argv[1], "dump", 4) == 0) return dump(argc, argv);
     if (argc < 3) {
-        fprintf(stderr, "usage: jni_harness cpu|gpu <sstable.bin> [log]\n");
+        fprintf(stderr, "usage: jni_harness cpu|gpu <sstable.bin> [log]\n"
+                        "       jni_harness dump|dump-default <out> table <sst> | tables <sst>... | log <log> <0|1>\n");
         return 2;
     }
     const int gpu = strcmp(argv[1], "gpu") == 0;

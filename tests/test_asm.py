@@ -28,7 +28,7 @@ def asm(tmp_path_factory):
     def one(i):
         src, defs = UNITS[i]
         out = d / f"u{i}.s"
-        # the study build: the product kernels and every superseded / debug variant
+        # the study build: the product kernels and the gv4 bound-study variants
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed",
                         "--cuda-device-only", "-S", "-DJL_STUDY=1", *defs, "-o", str(out), os.path.join(CSRC, src)],
                        check=True, capture_output=True)
@@ -50,10 +50,10 @@ def test_no_stale_ring_reads(asm):
 
     ks = {s: b for s, b in kernels(asm).items() if "crc_" in s}
     assert sum("crc_stream_kernel" in s for s in ks) >= 15
-    assert any("crc_fixed4k_x2" in s for s in ks) and any("crc_fixed4k_v4" in s for s in ks)
+    assert any("crc_fixed4k_v4" in s for s in ks)
     assert sum("crc_gv4_kernel" in s for s in ks) >= 4
     assert any("crc_logstream_kernel" in s for s in ks)
-    branchy = ("crc_stream_kernel", "crc_general_kernel")
+    branchy = ("crc_stream_kernel",)
 
     def one(s, b):
         if "crc_gv4_kernel" in s:

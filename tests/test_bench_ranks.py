@@ -2,7 +2,7 @@
 (`--same-device`: every rank on GPU 0, gloo collectives): the spawn through
 torch.distributed.run from a parent that never initialises HIP, the barriers,
 the MAX-over-ranks timing, the padded all-gather of unequal strong shards, and
-rank 0's single JSON line with n_gpus = 2 — plus the gathered results equal to
+rank 0's single JSON line with n_gpus = 2 and 8 (the driver's largest N) — plus the gathered results equal to
 one launch over the whole set (BASELINE config C4's shape, DBBench.java:775-793
 blocks), recorded on the line as parity_gathered_vs_single_launch.  What the
 driver's 8-GPU run adds is RCCL instead of gloo and one GPU per rank.
@@ -17,8 +17,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(*extra):
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--steps", "2",
+def _bench(*extra, gpus=2):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--same-device", "--steps", "2",
            "--warmup", "1", "--settle-ms", "0", "--no-cpu", "--no-secondary", *extra]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -35,6 +35,29 @@ def test_bench_two_ranks_weak():
     assert r["config"]["blocks_per_gpu"] == 4096
     assert r["parity_gathered_vs_single_launch"] is True
     assert r["value"] > 0 and r["result_allgather_ms"] is not None
+    assert len(r["rank_kernel_ms"]) == 2 and r["rank_kernel_ms_spread"] >= 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_eight_ranks_weak():
+    """The driver's N = 8 launch shape (C4 weak, 1M blocks per GPU there; 4096
+    here, 8 ranks sharing GPU 0): 8 processes through torch.distributed.run."""
+    r = _bench("--blocks", "4096", gpus=8)
+    assert r["n_gpus"] == 8 and r["scaling"] == "weak" and r["config"]["blocks_per_gpu"] == 4096
+    assert r["parity_gathered_vs_single_launch"] is True
+    assert len(r["rank_kernel_ms"]) == 8 and max(r["rank_kernel_ms"]) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_bench_eight_ranks_strong():
+    """C4 strong over 8 ranks with a total that does not divide (65541 = 8 x 8192
+    + 5: ranks 0-4 one block longer)."""
+    r = _bench("--strong-total", "65541", gpus=8)
+    assert r["n_gpus"] == 8 and r["scaling"] == "strong"
+    assert r["config"]["blocks_per_gpu"] == 8193
+    assert r["parity_gathered_vs_single_launch"] is True
 
 
 @pytest.mark.gpu

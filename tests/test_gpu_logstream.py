@@ -176,3 +176,30 @@ def test_dense_blocks(gpu, jl, oracle, case):
     log = bytes(log)
     want = _check(jl, oracle, log, read_records=True)
     assert len(want) > 65
+
+
+@pytest.mark.parametrize("shift", [1, 3, 8, 15])
+def test_dense_blocks_unaligned_log(gpu, jl, oracle, shift):
+    """lc_dense's byte-staging path: a log that does not start on 16 bytes (a
+    device view at byte offset `shift`) stages every block bytewise, not only the
+    short last one; DBBench-shaped records (every block dense) with flips, full
+    events against the oracle (dropped records included)."""
+    import torch
+
+    from jleveldb_amd import workloads
+
+    rng = np.random.default_rng(300 + shift)
+    log = bytearray(oracle.log_write(_payloads(rng, [workloads.DBBENCH_PAYLOAD] * (6 * 32768 // 138 + 17))))
+    for _ in range(5):
+        log[int(rng.integers(0, len(log)))] ^= 1 << int(rng.integers(0, 8))
+    host = np.zeros(len(log) + 16, np.uint8)
+    host[shift:shift + len(log)] = np.frombuffer(bytes(log), np.uint8)
+    d = torch.from_numpy(host).to(gpu)[shift:shift + len(log)]
+    assert d.data_ptr() % 16 == shift % 16
+    want = oracle.log_events(bytes(log))
+    for mode in (1, TWO_PASS):
+        ev, n = jl.log_verify_dev(d, mode)
+        got = ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)
+        assert n == want.size
+        for f in ("offset", "length", "type", "kind"):
+            assert np.array_equal(got[f], want[f]), (mode, f)

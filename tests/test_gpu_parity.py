@@ -36,20 +36,10 @@ def test_fixed_4k_random(gpu, jl, oracle, n_blocks):
     assert np.array_equal(raw, oracle.fixed(host, 4096, n_blocks, flags=0, threads=THREADS))
 
 
-FIXED_VARIANTS = {"x2": "3", "x2plain": "2", "v4_8": "7", "v4_16": "8", "v4_8_plain": "10", "v4_8_p8_512": "11",
-                  "v4_8_p16_512": "12", "v4_8_p16": "13"}
-
-
-@pytest.mark.parametrize("variant", sorted(FIXED_VARIANTS))
 @pytest.mark.parametrize("n_blocks", [1, 7, 8, 9, 63, 64, 65, 1000, 16385, 65536 + 13])
-def test_fixed_4k_kernel_variants(gpu, jl, oracle, engine_options, variant, n_blocks):
-    """The 4 KiB product kernel (v4_8) — and in a study build (make STUDY=1) every
-    superseded variant (JL_OPT_FIXED_KERNEL) — at ragged counts around the round
-    (8/4 blocks), group (64 blocks) and grid boundaries."""
-    if variant != "v4_8":
-        if "study build" not in jl.version():
-            pytest.skip("superseded 4 KiB kernel: study build only")
-        engine_options(jl.OPT_FIXED_KERNEL, int(FIXED_VARIANTS[variant]))
+def test_fixed_4k_ragged(gpu, jl, oracle, n_blocks):
+    """The 4 KiB kernel at ragged counts around the round (8 blocks), group (64
+    blocks) and grid boundaries, masked and raw."""
     rng = np.random.default_rng(1000 + n_blocks)
     host = rng.integers(0, 256, n_blocks * 4096, dtype=np.uint8)
     d = to_dev(host, gpu)

@@ -193,6 +193,36 @@ def test_async_then_host_call_share_scratch(gpu, jl, oracle, log_image):
     assert np.array_equal(_live(got_h), _live(oracle.log_events(host)))
 
 
+def test_async_then_empty_sync_call_then_device_call(gpu, jl, oracle, log_image):
+    """An async verification in flight on the null stream, then an EMPTY
+    synchronous jl_log_verify_dev on a side stream (it returns before any launch,
+    so it never waits for the async call), then a device-path jl_log_verify_dev of
+    another log on a third stream: the third call must still wait for the async
+    one before it reuses the thread's scratch (empty WAL / MANIFEST files are
+    common in a batch of logs).  Both results equal the oracle's."""
+    import torch
+
+    a = torch.from_numpy(log_image[: 96 << 20].copy()).to(gpu)
+    b = torch.from_numpy(log_image[CH: CH + (80 << 20)].copy()).to(gpu)
+    empty = torch.zeros(16, dtype=torch.uint8, device=gpu)
+    ev = torch.zeros((a.numel() // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    assert torch.cuda.current_stream().cuda_stream == 0  # the null stream
+    _, res = jl.log_verify_dev_async(a, events=ev)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        _, n0 = jl.log_verify_dev(empty[:0])
+    assert n0 == 0
+    with torch.cuda.stream(s2):
+        ev2, n2 = jl.log_verify_dev(b)
+    torch.cuda.synchronize()
+    n = int(res.cpu()[0])
+    assert np.array_equal(_live(ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)),
+                          _live(oracle.log_events(log_image[: 96 << 20])))
+    assert np.array_equal(_live(ev2[: n2 * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)),
+                          _live(oracle.log_events(log_image[CH: CH + (80 << 20)])))
+
+
 @pytest.mark.parametrize("mode", ["staged", "pinned"])
 def test_dense_log_host(gpu, jl, oracle, engine_options, mode):
     """~150 MiB DBBench-default log (131-B payloads: every 32 KiB block dense) with

@@ -22,9 +22,7 @@ out = torch.empty(n, dtype=torch.int32, device="cuda")
 sink = torch.zeros(1, dtype=torch.int32, device="cuda")
 kinds = os.environ.get("KINDS", "crc7 stream").split()
 for kind in kinds:
-    if kind.startswith("crc"):  # crc7 = the product kernel; others need a study build (JLCRC_STUDY_LIB)
-        if kind != "crc7":
-            jl.set_option(jl.OPT_FIXED_KERNEL, int(kind[3:]))
+    if kind.startswith("crc"):  # crc7 = the product kernel (the r1 variants: branch study-superseded-kernels)
         fn = lambda: jl.crc32c_fixed_dev(data, 4096, out=out)  # noqa: E731
     else:
         fn = lambda: jl.read_stream_dev(data, sink)  # noqa: E731
