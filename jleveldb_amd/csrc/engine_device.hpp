@@ -76,6 +76,10 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 
 __device__ __forceinline__ uint32_t mask_crc(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+__device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {  // J/util/Crc32C.java:72-75
+    const uint32_t r = m - 0xa282ead8u;
+    return (r >> 17) | (r << 15);
+}
 
 __device__ __forceinline__ void load_image(uint32_t *lds, const uint4 *__restrict__ img) {
     uint4 *d = (uint4 *)lds;

@@ -4,7 +4,10 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -323,38 +326,106 @@ struct HostSrc {
     }
 };
 
-// memcpy split over up to JL_OPT_STAGE_THREADS threads (pageable -> pinned
-// staging runs at one core's copy rate otherwise, well under PCIe's)
-void par_memcpy(void *dst, const void *src, size_t n) {
-    const size_t piece = 4ull << 20;
-    const int t = (int)std::min<size_t>((size_t)std::max(1, opt().stage_threads), n / piece);
-    if (t <= 1) {
-        memcpy(dst, src, n);
-        return;
+// Persistent staging workers for pageable -> pinned copies (one core copies at
+// ~10-20 GB/s, well under PCIe's ~55): a copy is cut into 256 KiB pieces that
+// the caller and up to JL_OPT_STAGE_THREADS - 1 pool threads take from a shared
+// cursor.  Persistent threads, because starting threads per call (r3) cost more
+// than a one-table copy itself, so r3 copied anything under 4 MiB on one core.
+// Concurrent callers queue their copies; every caller also works on its own.
+class CopyPool {
+  public:
+    static constexpr size_t kPiece = 256u << 10;
+    void copy(void *dst, const void *src, size_t n, int threads) {
+        if (n < 2 * kPiece || threads <= 1) {
+            memcpy(dst, src, n);
+            return;
+        }
+        Job j{(char *)dst, (const char *)src, n, (n + kPiece - 1) / kPiece};
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            while ((int)th_.size() < threads - 1 && (int)th_.size() < 63) th_.emplace_back([this] { work(); });
+            q_.push_back(&j);
+        }
+        cv_.notify_all();
+        run(j);  // the caller copies too, then waits for the pieces others took
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return j.left.load() == 0; });
     }
-    const size_t per = ((n + t - 1) / t + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    for (int i = 1; i < t && (size_t)i * per < n; i++) {
-        const size_t a = (size_t)i * per, b = std::min(n, a + per);
-        th.emplace_back([=] { memcpy((char *)dst + a, (const char *)src + a, b - a); });
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
     }
-    memcpy(dst, src, std::min(n, per));
-    for (auto &x : th) x.join();
+
+  private:
+    struct Job {
+        char *dst;
+        const char *src;
+        size_t n, pieces;
+        std::atomic<size_t> next{0}, left{0};
+        Job(char *d, const char *s, size_t n_, size_t p) : dst(d), src(s), n(n_), pieces(p) { left = p; }
+    };
+    void run(Job &j) {  // copies pieces of j until none is left to take
+        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces;) {
+            const size_t a = i * kPiece, b = std::min(j.n, a + kPiece);
+            memcpy(j.dst + a, j.src + a, b - a);
+            if (j.left.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> lk(mu_);
+                done_.notify_all();
+            }
+        }
+    }
+    void work() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (stop_) return;
+            Job *j = q_.front();
+            if (j->next.load() >= j->pieces) {  // every piece taken: the job leaves the queue
+                q_.pop_front();
+                continue;
+            }
+            lk.unlock();
+            run(*j);  // j outlives this: its caller waits until every piece is done
+            lk.lock();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::deque<Job *> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
+CopyPool &copy_pool() {
+    static CopyPool *p = new CopyPool;  // never destroyed: workers may outlive static destruction order
+    return *p;
 }
+void par_memcpy(void *dst, const void *src, size_t n) { copy_pool().copy(dst, src, n, std::max(1, opt().stage_threads)); }
 
 // Enqueues the copy of src.p[off, off + bytes) into sl.d_in on the slot's copy
 // stream, after the slot's previous use; staged through pinned memory when the
 // source is pageable.
+// A pageable source is staged in pieces of kStagePiece, each DMA'd as soon as it
+// is in pinned memory, so the copy engine works on piece i while the host copies
+// piece i + 1 (one call's latency is then about the host copy, not copy + DMA).
+constexpr uint64_t kStagePiece = 1ull << 20;
 int slot_put_data(Slot &sl, const HostSrc &src, uint64_t off, uint64_t bytes) {
     JL_HIP(hipStreamWaitEvent(sl.st, sl.used, 0));
     const uint8_t *p = src.p + off;
-    if (!src.direct) {
-        JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
-        JL_HIP(sl.h_data.ensure(bytes));
-        par_memcpy(sl.h_data.p, p, bytes);
-        p = (const uint8_t *)sl.h_data.p;
+    if (src.direct) {
+        if (bytes) JL_HIP(hipMemcpyAsync(sl.d_in.p, p, bytes, hipMemcpyHostToDevice, sl.st));
+        return JL_OK;
     }
-    if (bytes) JL_HIP(hipMemcpyAsync(sl.d_in.p, p, bytes, hipMemcpyHostToDevice, sl.st));
+    JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
+    JL_HIP(sl.h_data.ensure(bytes));
+    for (uint64_t a = 0; a < bytes; a += kStagePiece) {
+        const uint64_t m = std::min(kStagePiece, bytes - a);
+        par_memcpy((uint8_t *)sl.h_data.p + a, p + a, m);
+        JL_HIP(hipMemcpyAsync((uint8_t *)sl.d_in.p + a, (const uint8_t *)sl.h_data.p + a, m, hipMemcpyHostToDevice, sl.st));
+    }
     return JL_OK;
 }
 
@@ -387,12 +458,29 @@ int slot_put_desc(Slot &sl, std::initializer_list<Part> parts) {
     return JL_OK;
 }
 
+// Waits for the stream's work: polls it (hipStreamQuery) for up to kPollSpinUs,
+// then polls yielding the core to other threads up to kPollYieldUs, then blocks.
+// A log verification of a few MiB returns without the ~50 us wake-up of a
+// blocking synchronise (r2: 0.93 -> 0.88 ms on C5), and concurrent callers do
+// not each keep a host core spinning for long.
+constexpr double kPollSpinUs = 200.0, kPollYieldUs = 5000.0;
+hipError_t poll_stream(hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (us > kPollYieldUs) return hipStreamSynchronize(st);
+        if (us > kPollSpinUs) std::this_thread::yield();
+    }
+}
+
 // Waits for both pipelines' work to finish and returns the first error of the
 // call, if any.
 int drain(Workspace &w, int rc) {
-    hipError_t e = hipStreamSynchronize(w.stream);
+    hipError_t e = poll_stream(w.stream);  // a short call returns without a blocking wake-up
     for (Slot &sl : w.slot) {
-        hipError_t f = hipStreamSynchronize(sl.st);
+        hipError_t f = poll_stream(sl.st);
         if (e == hipSuccess) e = f;
     }
     if (rc) return rc;
@@ -1205,23 +1293,6 @@ static int log_verify_stream(Workspace &c, const void *d_log, uint64_t log_bytes
 // stream-ordered, one pass for any log: the round table is sized for at most
 // kLCSlots events per 32 KiB block (records of ~500 B and up), and the blocks
 // of more events (dense) are verified whole by lc_dense instead.
-// Waits for the stream's work: polls it (hipStreamQuery) for up to kPollSpinUs,
-// then polls yielding the core to other threads up to kPollYieldUs, then blocks.
-// A log verification of a few MiB returns without the ~50 us wake-up of a
-// blocking synchronise (r2: 0.93 -> 0.88 ms on C5), and concurrent callers do
-// not each keep a host core spinning for long.
-constexpr double kPollSpinUs = 200.0, kPollYieldUs = 5000.0;
-static hipError_t poll_stream(hipStream_t st) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        const hipError_t e = hipStreamQuery(st);
-        if (e != hipErrorNotReady) return e;
-        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-        if (us > kPollYieldUs) return hipStreamSynchronize(st);
-        if (us > kPollSpinUs) std::this_thread::yield();
-    }
-}
-
 // d_result null: synchronous (the count read back); else asynchronous: the
 // result words go to d_result on the stream and the call returns after the
 // launches.
@@ -1237,17 +1308,20 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_end = o_res + 256;
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
-    // the dense blocks' events: at most the caller's capacity (more events fail the call anyway).
-    // With pools (>= 8 blocks per lc_dense workgroup) a workgroup leaves less than a pool
-    // unused at the end, and less than its next block's events (<= kLDMaxEv) per refill:
-    // refills <= events / (pool - kLDMaxEv) + grid
+    // The dense blocks' runs of events (lc_dense): no more runs than events, and
+    // at most the caller's capacity of events (more fail the call anyway), plus one
+    // link entry per pass after a block's first (a pass holds kLDRuns runs, so
+    // links <= runs / kLDRuns).  With pools (>= 8 blocks per lc_dense workgroup) a
+    // workgroup leaves less than a pool unused at the end and fewer than
+    // kLDRuns + 1 entries per refill: refills <= entries / (pool - kLDRuns - 1) + grid.
     // A count-only call (no event array) stashes nothing: lc_dense skips the stores
-    // of a block that does not fit (stash_cap 0), and lc_build has no events to write.
-    const uint64_t need = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
+    // of a pass that does not fit (stash_cap 0), and lc_build has no events to write.
+    const uint64_t need0 = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
+    const uint64_t need = need0 + need0 / jlk::kLDRuns;
     const uint64_t grid = jlk::lc_dense_grid(ctx().cus);
     const uint64_t pool = need && nb >= 8 * grid ? jlk::kLDPool : 0;
     const uint64_t stash_cap =
-        pool ? need + (need / (pool - jlk::kLDMaxEv) + grid) * jlk::kLDMaxEv + grid * pool : need;
+        pool ? need + (need / (pool - jlk::kLDRuns - 1) + grid) * (jlk::kLDRuns + 1) + grid * pool : need;
     JL_HIP(c.ws_stash.ensure(std::max<uint64_t>(stash_cap, 1) * 8));
     char *ws = (char *)c.ws_lc.p;
     jlk::LCArgs A;
@@ -1275,6 +1349,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.ev = (jlk::LogEvent *)d_events;
     A.ev_cap = d_events ? cap : 0;
     A.aux = ctx().d_aux;
+    A.seed0 = jlmath::slice4_inv(0xffffffffu);
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
     JL_HIP(jlk::launch_lc_walk(A, st));

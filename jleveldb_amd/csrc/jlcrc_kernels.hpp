@@ -125,7 +125,7 @@ constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk r
 constexpr uint32_t kLCSlots = 64;
 constexpr uint32_t kLCProbe = 8;
 constexpr uint32_t kLCDense = 0xffffffffu;  // count[b] of a dense block until lc_dense counts it
-constexpr uint32_t kLDMaxEv = 4688;         // >= events of one 32 KiB block (one per 7 bytes)
+constexpr uint32_t kLDMaxEv = 4688;         // >= events (and runs) of one 32 KiB block (one per 7 bytes)
 constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
 struct LCBig {        // a record of more than one chunk
     uint64_t p;       // crc range start (h + 6) relative to the log
@@ -141,16 +141,18 @@ struct LCArgs {
     int checksum;
     uint64_t *slots;       // n_blocks * kLCSlots walked events: length | type << 16 | kind << 24 | stored << 32
     uint32_t *count;       // n_blocks + 1 (count[n_blocks] = 0); dense blocks: see kLCDense
-    // dense blocks' events, 8 B each (offset in block | length << 16 | type << 32 |
-    // kind << 40), block b's run at stash[dense_off[b]] (dense_off: kLCNotDense for
-    // the other blocks, written by lc_walk; ~0 for a dense block whose run did not
-    // fit: the caller's event array is too small anyway)
+    // dense blocks' RUNS of events, 8 B each (offset in block | length << 16 | count
+    // << 32 | type << 48 | kind << 56), block b's first stash segment at
+    // dense_off[b] = stash offset | entries << 48; a segment's last entry may link
+    // to the next one (kind 0xff: stash offset | entries << 40).  dense_off is
+    // kLCNotDense for the other blocks (lc_walk), ~0 for a dense block whose runs
+    // did not fit (the caller's event array is too small anyway)
     uint64_t *dense_off;
     uint64_t *stash;
     uint64_t stash_cap;
-    // > 0: a workgroup takes stash entries stash_pool at a time (>= kLDMaxEv; one
+    // > 0: a workgroup takes stash entries stash_pool at a time (> kLDRuns; one
     // atomic per many blocks, whose wait would also wait for the prefetch loads);
-    // 0: one atomic per block (small logs)
+    // 0: one atomic per pass (small logs)
     uint64_t stash_pool;
     unsigned long long *stash_ctr;  // zeroed by lc_walk
     uint64_t *start;       // n_blocks + 1: exclusive scan of count
@@ -158,6 +160,7 @@ struct LCArgs {
     uint32_t *hscan;       // its exclusive scan
     uint32_t *rstart;      // kLCBins + 1: first round of every bin; [kLCBins] = rounds
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
+    uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range
     uint32_t *cap_flag;    // set when a capacity was exceeded
     uint64_t *result;      // [0] events, [1] dense blocks, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8
@@ -178,6 +181,7 @@ hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
 uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
+constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
 
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)

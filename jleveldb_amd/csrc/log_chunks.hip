@@ -128,17 +128,14 @@ __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
 }
 // the walk's hop load (lc_walk): lc_header's bytes with JL_LC_HDR_POLICY (an asm load,
 // waited for at once: the hop is a dependent chain anyway)
-// Study switches (0 in the product): non-temporal stores of the events / round
-// descriptors / stash and loads of the stash (JL_NT_EV), and lc_dense's block
-// staging loads (JL_NT_STAGE).  r3 same-box A/B (tools/ab_lib.sh, C5 sets
-// mixed / 1 056-B / DBBench, ms): product 0.82 / 1.014 / 1.59, JL_NT_EV 0.825 /
-// 1.035 / 1.587 (gv4 then reads its descriptors from HBM), JL_NT_STAGE 0.826 /
-// 1.02 / 1.62, both 0.845 / 1.032 / 1.588: not kept.
+// Study switch (0 in the product): non-temporal stores of the events / round
+// descriptors and loads of the stash (JL_NT_EV).  r3 same-box A/B
+// (tools/ab_lib.sh, C5 sets mixed / 1 056-B / DBBench, ms): product 0.82 /
+// 1.014 / 1.59, JL_NT_EV 0.825 / 1.035 / 1.587 (gv4 then reads its descriptors
+// from HBM); non-temporal staging loads in r3's lc_dense 0.826 / 1.02 / 1.62:
+// not kept.
 #ifndef JL_NT_EV
 #define JL_NT_EV 0
-#endif
-#ifndef JL_NT_STAGE
-#define JL_NT_STAGE 0
 #endif
 typedef uint32_t lc_v4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void lc_st16(void *p, lc_v4 v) {
@@ -333,6 +330,7 @@ __device__ __forceinline__ void lc_desc(const LCArgs &A, const uint32_t *rs, uin
 }
 
 __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v);
+constexpr uint32_t kLDLinkKind = 0xffu;  // stash entry kind of a segment link (lc_dense)
 
 // The chunk descriptors of one OK record per lane (ok false: none), all lanes
 // calling.  Ranks come from LDS atomics per lane: with bins by (K, d mod 16) a
@@ -429,6 +427,56 @@ __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
     return x - v;
 }
 
+// A dense block's events from its runs (lc_dense's stash segments): a wave takes
+// 64 runs at a time (lane = run: its count, exclusive prefix over the lanes),
+// then writes their events 64 at a time, lane = event, each finding its run by
+// a binary search over the lanes' prefixes.  Event k of a run: header at offset
+// + k (7 + length).
+__device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint64_t ev0, uint64_t doff) {
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    uint64_t so = doff & 0xffffffffffffull;
+    uint32_t n = (uint32_t)(doff >> 48);
+    uint64_t k0 = 0;  // events of the block written so far
+    while (n) {
+        uint32_t nn = 0;  // the next segment (a link in this one's last entry)
+        uint64_t sn = 0;
+        for (uint32_t r0 = 0; r0 < n; r0 += 64u) {
+            const uint64_t e = r0 + lane < n ? lc_ld8(&A.stash[so + r0 + lane]) : 0ull;
+            const bool link = r0 + lane < n && (e >> 56) == kLDLinkKind;
+            const uint64_t lb = __builtin_amdgcn_ballot_w64(link);
+            if (lb) {
+                const uint32_t src = (uint32_t)__builtin_ctzll(lb);
+                const uint64_t le = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(e >> 32), (int)src) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)e, (int)src);
+                sn = le & 0xffffffffffull;
+                nn = (uint32_t)(le >> 40) & 0xffffu;
+            }
+            const uint32_t cnt = r0 + lane < n && !link ? (uint32_t)(e >> 32) & 0xffffu : 0u;
+            const uint32_t ex = lc_wave_excl_sum(cnt);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)(ex + cnt), 63);
+            for (uint32_t c0 = 0; c0 < tot; c0 += 64u) {
+                const uint32_t c = c0 + lane;
+                uint32_t o = 0;  // the last lane whose prefix is <= c: event c's run
+                for (uint32_t s = 32u; s; s >>= 1) {
+                    const uint32_t cand = o + s;
+                    if ((uint32_t)__shfl((int)ex, (int)cand) <= c) o = cand;
+                }
+                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)e, (int)o);
+                const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(e >> 32), (int)o);
+                const uint32_t eo = (uint32_t)__shfl((int)ex, (int)o);
+                if (c < tot) {
+                    const uint32_t len = lo >> 16;
+                    lc_event(A, ev0 + k0 + c, b * 32768u + (lo & 0xffffu) + (uint64_t)(c - eo) * (7u + len), len,
+                             (hi >> 16) & 0xffu, hi >> 24);
+                }
+            }
+            k0 += tot;
+        }
+        so = sn;
+        n = nn;
+    }
+}
+
 __device__ __forceinline__ void lc_finish(const LCArgs &A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.result[0] = A.start[A.n_blocks];
@@ -465,25 +513,9 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         if (b >= A.n_blocks) break;
         const uint64_t doff = A.dense_off[b];
-        if (doff != kLCNotDense) {  // dense block: its events from the stash (lc_dense)
+        if (doff != kLCNotDense) {  // dense block: its events expanded from lc_dense's runs
             if (doff == ~0ull) continue;  // did not fit: the event array is too small anyway
-            // 4 loads in flight per lane before the stores (the compiler cannot move a
-            // stash load above an event store: it does not know they do not alias)
-            for (uint32_t k0 = 0; k0 < cnt[i]; k0 += 256u) {
-                uint64_t e[4];
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t k = k0 + lane + 64u * j;
-                    e[j] = k < cnt[i] ? lc_ld8(&A.stash[doff + k]) : 0ull;
-                }
-#pragma unroll
-                for (uint32_t j = 0; j < 4; j++) {
-                    const uint32_t k = k0 + lane + 64u * j;
-                    if (k < cnt[i])
-                        lc_event(A, st[i] + k, b * 32768u + (e[j] & 0xffffu), (uint32_t)(e[j] >> 16) & 0xffffu,
-                                 (uint32_t)(e[j] >> 32) & 0xffu, (uint32_t)(e[j] >> 40) & 0xffu);
-                }
-            }
+            lc_expand_runs(A, b, st[i], doff);
             continue;
         }
         const uint64_t bs = b * 32768u, s = sl[i];
@@ -555,24 +587,33 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // Dense blocks (lc_walk's kLCDense: records of ~500 B and less, e.g. DBBench's
 // default 100-B values make ~237 records of 138 B per 32 KiB block).  Cutting
 // them into 8-chunk rounds would pay a round epilogue per ~2 windows, so a
-// workgroup takes the whole block instead: it stages the block in LDS, walks
-// its headers there, checks every record's crc with one thread per record
-// (kLDSlice / 4 interleaved slicing chains from LDS tables) and stashes the block's events in file order
-// (8 B each) with its exact event count, before the event scan; lc_build copies
-// them to their places.  Persistent grid over the blocks lc_walk marked; each
-// workgroup loads its next dense block into registers while it works on the
-// current one.
-//
-// The walk (one wave) speculates: on the stride L = 7 + n of the last run, lane
-// k reads the headers at p + (k + 64 j) L, j < kLDCand, in the same LDS trip as
-// the header at p itself; the candidates up to the first one that is not an OK
-// record of the same length are the next headers of the chain (the reference's
-// decisions in its order, J/db/LogReader.java:297-383).  A run of equal records
-// is walked 256 headers per LDS round trip; a new length costs a second trip.
-//
-// Tables: kLDRep copies of T0..T_{kLDSlice-1} interleaved so that copy r sits in banks
-// {r, r + kLDRep, ...} and thread t reads copy t mod kLDRep: the random lookups
-// of 32 lanes conflict only among the 32 / kLDRep lanes sharing a copy.
+// workgroup takes the whole block instead (persistent grid over the blocks
+// lc_walk marked, 3 workgroups of 256 threads per CU; the next dense block's
+// 32 KiB load into registers while the current one is worked on):
+//   stage  the block into LDS
+//   walk   RUNS of records: the header at p is read by every thread, thread t
+//          checks the candidate header at p + (t + 1) L (L = 7 + its length) —
+//          an OK record of the same length and type — and the first failing
+//          candidate (ballot, LDS min) ends the run: a run of equal records
+//          (DBBench's) is walked 257 headers per trip, one barrier each
+//          (J/db/LogReader.java:297-383, the reference's decisions in its order)
+//   crc    one thread per OK record, table lookups that never conflict: the
+//          state advances a dword at a time through 8 nibble tables
+//          N_i[v] = z^4(v << 4i), 32 copies interleaved so lane l reads bank
+//          l mod 32 (r3's byte tables, one copy beside the staged block, spent
+//          58 % of the LDS cycles in bank conflicts, profiles/r3n_pmc_lc_dense.json);
+//          the record's first bytes are seeded with W0 (the 4 bytes before it
+//          that take state 0 to value()'s 0xffffffff, so the first dword needs
+//          no byte tables), its last dword is zero-padded and the stored crc
+//          shifted over the same zeros instead; a failure atomicMin's its header
+//          offset into first_bad[block] (lc_apply turns it into BAD_CRC and the
+//          rest of the block into drops, :359-367, as for the other blocks)
+//   stash  the block's runs (8 B each: offset, length, count, type, kind), not
+//          its events: lc_build expands them into the event array
+// A pass holds kLDRuns runs; a block of more (hundreds of short records of
+// changing lengths) takes several passes, their stash segments chained by a
+// link entry in the last slot of each.
+constexpr uint32_t kLDThreads = 256;
 __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
     return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
 }
@@ -580,84 +621,26 @@ __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // 
 __device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uint32_t c) {
     return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
 }
-#ifndef JL_LD_CAND
-#define JL_LD_CAND 1  // r3n A/B (DBBench set): 1 1.62 ms, 2 1.64, 4 1.73 (more LDS reads per trip);
-                      // r3: speculating after a lone record on the last long run's stride
-                      // (kept across blocks) 1.589 vs 1.575 ms: a first trip of 64 distinct
-                      // reads instead of one broadcast costs more than the reload it saves
-#endif
-constexpr uint32_t kLDCand = JL_LD_CAND;  // walk candidates per lane and LDS trip
-
-// A/B on the DBBench set (whole verification, tools/ab_lib.sh): r3f, slicing-by-4,
-// before the LDS-only barrier: 1.99 ms (2 copies, 3 workgroups per CU) vs 2.21 (4)
-// and 2.16 (8, both 2 per CU); r3j, LDS-only barrier and stash pools: 1.585 ms
-// (slicing 8, 1 copy, 3 per CU) vs 1.72 (4, 2 copies, 3 per CU), 1.94 (16, 1 copy,
-// 2 per CU) and 2.03 (8, 2 copies, 2 per CU); r3o, two threads per record (front
-// and back 64 B, folded with z^64; 512 threads): 1.70 / 2.24 ms vs 1.61.  PMC
-// r3n: LDS busy ~68 % of the kernel, 58 % of that bank conflicts of the random
-// lookups (one copy), VALU ~30 %: the lookups' LDS cycles bound it, not the
-// length of a record's dependence chain
-#ifndef JL_LD_REP
-#define JL_LD_REP 1
-#endif
-#ifndef JL_LD_HLCAP
-#define JL_LD_HLCAP kLDMaxEv  // study: a smaller header buffer (only for logs of <= this many events per block)
-#endif
-// r3 (JL_LD_HLCAP 2048 keeps 3 workgroups per CU with 2 table copies): DBBench set
-// 1.561 ms (product) vs 1.645 (2 copies, 3 per CU) and 2.00 (4 copies, 2 per CU)
-// Slicing width: a record's dwords go round-robin to kLDSlice / 4 independent
-// chains, each advancing kLDSlice bytes per step through T_{S-1}..T_{S-4}, so the
-// dependent LDS round trips per record drop from one per 4 B to one per S bytes
-#ifndef JL_LD_SLICE
-#define JL_LD_SLICE 8
-#endif
-constexpr uint32_t kLDThreads = 256, kLDRep = JL_LD_REP, kLDSlice = JL_LD_SLICE, kLDChains = kLDSlice / 4;
-static_assert(kLDSlice == 4 || kLDSlice == 8 || kLDSlice == 12 || kLDSlice == 16, "slicing width");
-static_assert(kLDPool >= kLDMaxEv, "a fresh stash pool holds any block");
-// T_k[e] (e followed by k zero bytes), this thread's copy
-__device__ __forceinline__ uint32_t ld_t(const uint32_t *T, uint32_t k, uint32_t e) { return T[(256u * k + e) * kLDRep]; }
-// the dword x (the state xor the next 4 data bytes) followed by n - 4 zero bytes
-__device__ __forceinline__ uint32_t ld_adv(const uint32_t *T, uint32_t x, uint32_t n) {
-    return xor3(ld_t(T, n - 1u, x & 0xffu), ld_t(T, n - 2u, (x >> 8) & 0xffu), ld_t(T, n - 3u, (x >> 16) & 0xffu)) ^
-           ld_t(T, n - 4u, x >> 24);
-}
-// k = 1..3 data bytes v (low bytes) into the state x: one round trip
-__device__ __forceinline__ uint32_t ld_absorb(const uint32_t *T, uint32_t x, uint32_t v, uint32_t k) {
-    const uint32_t y = x ^ v;
-    uint32_t r = (x >> (8u * k)) ^ ld_t(T, k - 1u, y & 0xffu);
-    if (k > 1u) r ^= ld_t(T, k - 2u, (y >> 8) & 0xffu);
-    if (k > 2u) r ^= ld_t(T, 0u, (y >> 16) & 0xffu);
-    return r;
-}
-// crc32c state over bytes [q, e) of the staged block from state x
-__device__ __forceinline__ uint32_t ld_crc(const uint32_t *T, const uint32_t *dat, uint32_t x, uint32_t q, uint32_t e) {
-    uint32_t k = (4u - (q & 3u)) & 3u;  // head: up to the next dword
-    if (k > e - q) k = e - q;
-    if (k) {
-        x = ld_absorb(T, x, (dat[q >> 2] >> (8u * (q & 3u))) & ((1u << (8u * k)) - 1u), k);
-        q += k;
+// z^4(x) ^ w (x: the state XORed with the next 4 data bytes; z^4: 4 zero bytes)
+// from the nibble tables N_i[v] = z^4(v << 4i).  Layout: tables 2j and 2j + 1
+// share a 4 KiB block of 16 rows of 256 B, row v = 32 copies of N_2j[v] then 32
+// of N_2j+1[v]; lane l reads copy l mod 32, so every lookup of a wave hits 32
+// distinct banks.  The lookup address (v << 8 | half << 7 | 4 (l mod 32)) is one
+// v_perm_b32 of the nibbles spread one per byte (x & 0x0f0f0f0f, (x >> 4) & ...)
+// and lb (byte 0: 4 (l mod 32), byte 1: the same | 0x80): 11 VALU for 8 addresses.
+__device__ __forceinline__ uint32_t ld_z4(const uint32_t *nt, uint32_t lb, uint32_t x, uint32_t w = 0u) {
+    const uint32_t lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
+    uint32_t r[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; i++) {
+        const uint32_t sel = 0x0c0c0000u | ((i >> 1) << 8) | (4u + (i & 1u));
+        const uint32_t a = __builtin_amdgcn_perm(lb, i & 1u ? hi : lo, sel);
+        r[i] = *(const uint32_t *)((const char *)nt + 4096u * (i >> 1) + a);
     }
-    const uint32_t *D = dat + (q >> 2);
-    const uint32_t m = (e - q) >> 2, G = m / kLDChains;
-    if (G) {
-        uint32_t c[kLDChains];
-#pragma unroll
-        for (uint32_t j = 0; j < kLDChains; j++) c[j] = j ? 0u : x;
-        for (uint32_t g = 1; g < G; g++, D += kLDChains) {
-#pragma unroll
-            for (uint32_t j = 0; j < kLDChains; j++) c[j] = ld_adv(T, c[j] ^ D[j], kLDSlice);
-        }
-        // the last step of chain j stops at the group's end: kLDSlice - 4 j bytes
-        x = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kLDChains; j++) x ^= ld_adv(T, c[j] ^ D[j], kLDSlice - 4u * j);
-        D += kLDChains;
-    }
-    for (uint32_t j = G * kLDChains; j < m; j++) x = ld_adv(T, x ^ *D++, 4u);
-    q += 4u * m;
-    if (q < e) x = ld_absorb(T, x, dat[q >> 2] & ((1u << (8u * (e - q))) - 1u), e - q);
-    return x;
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], w));
 }
+// z(s) through T0 (one zero byte)
+__device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { return (s >> 8) ^ T0[s & 0xffu]; }
 // A workgroup's dense blocks: the candidates blockIdx.x + j * gridDim.x, 64 of
 // them per wave-wide load of count[] (the ballot of the dense ones is kept, so a
 // log of dense blocks costs one load per 64 blocks and a log without any costs
@@ -697,25 +680,14 @@ struct LDPre {
     ld_v4 a, b, c, d, e, f, g, h;
     __device__ __forceinline__ void load(const uint8_t *blk, uint32_t t) {
         const ld_v4 *s = (const ld_v4 *)blk + t;
-        if (JL_NT_STAGE) {
-            a = __builtin_nontemporal_load(s + 0 * kLDThreads);
-            b = __builtin_nontemporal_load(s + 1 * kLDThreads);
-            c = __builtin_nontemporal_load(s + 2 * kLDThreads);
-            d = __builtin_nontemporal_load(s + 3 * kLDThreads);
-            e = __builtin_nontemporal_load(s + 4 * kLDThreads);
-            f = __builtin_nontemporal_load(s + 5 * kLDThreads);
-            g = __builtin_nontemporal_load(s + 6 * kLDThreads);
-            h = __builtin_nontemporal_load(s + 7 * kLDThreads);
-        } else {
-            a = s[0 * kLDThreads];
-            b = s[1 * kLDThreads];
-            c = s[2 * kLDThreads];
-            d = s[3 * kLDThreads];
-            e = s[4 * kLDThreads];
-            f = s[5 * kLDThreads];
-            g = s[6 * kLDThreads];
-            h = s[7 * kLDThreads];
-        }
+        a = s[0 * kLDThreads];
+        b = s[1 * kLDThreads];
+        c = s[2 * kLDThreads];
+        d = s[3 * kLDThreads];
+        e = s[4 * kLDThreads];
+        f = s[5 * kLDThreads];
+        g = s[6 * kLDThreads];
+        h = s[7 * kLDThreads];
     }
     __device__ __forceinline__ void store(uint32_t *dat, uint32_t t) const {
         ld_v4 *d4 = (ld_v4 *)dat + t;
@@ -732,55 +704,60 @@ struct LDPre {
 
 // A barrier over LDS only.  __syncthreads() also waits for every outstanding
 // global access (vmcnt(0): gfx950 counts loads and stores together), which held
-// each block's walk until the next block's prefetch had landed (tools/ld_prof.py:
-// ~6 K of ~16 K clocks per block).
+// each block's walk until the next block's prefetch had landed (r3 shader-clock
+// phase counters: ~6 K of ~16 K clocks per block).
 __device__ __forceinline__ void ld_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-#ifndef JL_LD_PROF
-#define JL_LD_PROF 0  // study builds: per-phase shader clocks of lc_dense (tools/ld_prof.py)
-#endif
-#if JL_LD_PROF
-__device__ unsigned long long g_ld_prof[8];
-#define LD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define LD_T(v)
-#endif
+// stash entries: a run (offset in block | length << 16 | count << 32 | type << 48 |
+// kind << 56) or, last in a segment, the link to the block's next segment
+// (kLDLink << 56 | entries << 40 | stash offset)
+constexpr uint64_t kLDLink = kLDLinkKind;
+__device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint32_t cnt) {
+    return (uint64_t)ra | ((uint64_t)cnt << 32) | ((uint64_t)(rb >> 16) << 48);
+}
 
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
-    __shared__ uint32_t dat[8192 + 4];          // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t tab[kLDSlice * 256 * kLDRep];  // T_k[e] copy r at word (256 k + e) kLDRep + r
-    __shared__ uint16_t hl[JL_LD_HLCAP];        // header offsets of the block's events
-    __shared__ uint32_t s_n, s_bad;
-    __shared__ unsigned long long s_off;
-    const uint32_t t = threadIdx.x, lane = t & 63u, rep = t % kLDRep;
-    {  // T0 from aux (crc_math.hpp build_aux), T_k[e] = T_{k-1}[e] >> 8 ^ T0[T_{k-1}[e] & 0xff]
-        uint32_t v = A.aux[t];
-        for (uint32_t r = 0; r < kLDRep; r++) tab[t * kLDRep + r] = v;
-        for (uint32_t k = 1; k < kLDSlice; k++) {
-            v = (v >> 8) ^ A.aux[v & 0xffu];
-            for (uint32_t r = 0; r < kLDRep; r++) tab[(256u * k + t) * kLDRep + r] = v;
-        }
+    __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
+    __shared__ uint32_t nt[8 * 16 * 32];  // nibble tables N_i[v], 32 copies (bank = lane mod 32)
+    __shared__ uint32_t t0[256];
+    __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
+    __shared__ uint32_t run_b[kLDRuns];  // first event (of the pass) | type << 16 | kind << 24
+    __shared__ uint32_t s_m[3];          // per trip (mod 3): first failing candidate
+    __shared__ uint32_t s_bad;           // header offset of the block's first failing record
+    __shared__ unsigned long long s_seg;  // stash offset of the pass's segment (~0: did not fit)
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    t0[t] = A.aux[t];
+    if (t < 3) s_m[t] = kLCNone;
+    ld_sync();
+    for (uint32_t w = t; w < 8u * 16u * 32u; w += kLDThreads) {  // N_i[v] = z^4(v << 4i), layout at ld_z4
+        const uint32_t i = 2u * (w >> 10) + ((w >> 5) & 1u), v = (w >> 6) & 15u;
+        uint32_t s = v << (4u * i);
+        for (int k = 0; k < 4; k++) s = ld_z1(t0, s);
+        nt[w] = s;
     }
-    const uint32_t *T = tab + rep;
+    ld_sync();
+    const uint32_t lb = 4u * (lane & 31u) * 0x101u + 0x8000u;  // ld_z4's lane bytes
+    // the first dword of a record whose crc range starts q & 3 = h bytes into a
+    // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
+    // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
+    const uint32_t W0 = A.seed0;
+    const uint32_t C1 = ld_z4(nt, lb, W0 << 8), C2 = ld_z4(nt, lb, W0 << 16), C3 = ld_z4(nt, lb, W0 << 24);
     LDSched sch;
     sch.init(A);
     uint64_t b = sch.next(A);
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
-#if JL_LD_PROF
-    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0};
-#endif
+    uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
     while (b < A.n_blocks) {
-        LD_T(ta);
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
-        ld_sync();  // the previous block's readers of dat / hl / s_* are done
+        ld_sync();  // the previous block's readers of dat / runs / s_* are done
         if (ld_vec(A, b)) {
             pre.store(dat, t);
         } else {  // the file's short last block (or an unaligned log): bytes, nothing past its end
@@ -793,59 +770,94 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
         }
         if (t < 4) dat[8192 + t] = 0;
+        if (t == 0) s_bad = kLCNone;
         ld_sync();
-        LD_T(tb);
         const uint64_t bn = sch.next(A);  // its bytes load during this block's work
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
-        LD_T(tb2);
-        unsigned long long off = 0;
-        if (t < 64) {  // the walk, wave 0
-            uint32_t p = 0, n = 0, L = 0;  // L: the last run's stride (7 + length), 0 before the first
-            for (;;) {
-                // one LDS trip: the header at p (lane 0's first candidate) and, on the
-                // last run's stride, the kLDCand * 64 - 1 after it
-                uint32_t w[kLDCand];
-#pragma unroll
-                for (uint32_t j = 0; j < kLDCand; j++) w[j] = ld_hdr(dat, blen, p + (lane + 64u * j) * L);
-                const LCDecision d0 = lc_decide(blen - p, eof, __builtin_amdgcn_readfirstlane(w[0]));  // lane 0: the header at p
-                if (d0.kind == 0) break;  // the block's trailer: no event
-                if (d0.stop) {
-                    if (lane == 0) hl[n] = (uint16_t)p;
-                    n++;
+        uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
+        uint64_t seg0 = ~0ull;      // thread 0: the block's first segment (stash offset | entries << 48)
+        uint64_t link = ~0ull;      // thread 0: the previous segment's link slot
+        bool fit = true, done = false;
+        while (!done) {
+            // the block's failure so far: read before this pass's crc atomics can change it
+            const bool crc = A.checksum && s_bad == kLCNone;
+            // ---- walk: up to kLDRuns runs from p
+            uint32_t nr = 0, nev = 0;
+            while (nr < kLDRuns) {
+                const LCDecision d0 = lc_decide(blen - p, eof, ld_hdr(dat, blen, p));
+                if (d0.kind == 0) {  // the block's trailer: no event
+                    done = true;
                     break;
                 }
-                const uint32_t L0 = 7u + d0.length;
-                if (L0 != L) {  // a new run: its candidates (a second trip when any is in the block)
-                    L = L0;
-                    if (p + L < blen) {
-#pragma unroll
-                        for (uint32_t j = 0; j < kLDCand; j++) w[j] = ld_hdr(dat, blen, p + (lane + 64u * j) * L);
-                    }
-                }
-                uint32_t m = 64u * kLDCand;
-#pragma unroll
-                for (uint32_t j = kLDCand; j-- > 0;) {  // the first candidate that breaks the run
-                    const uint32_t k = lane + 64u * j, cand = p + k * L;
-                    bool ok = k == 0;
-                    if (k && cand < blen && blen - cand >= 7) {
-                        const LCDecision dk = lc_decide(blen - cand, eof, w[j]);
-                        ok = dk.kind == 1u && dk.length == d0.length;
+                uint32_t m = 1;
+                if (!d0.stop) {
+                    const uint32_t L = 7u + d0.length, c = p + (t + 1u) * L;
+                    bool ok = false;
+                    if (c < blen && blen - c >= 7u) {
+                        const LCDecision dk = lc_decide(blen - c, eof, lds32u(dat, c + 3u));
+                        ok = dk.kind == 1u && dk.length == d0.length && dk.type == d0.type;
                     }
                     const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
-                    if (nok) m = 64u * j + (uint32_t)__builtin_ctzll(nok);
+                    const uint32_t slot = trip % 3u;
+                    if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
+                    if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
+                    ld_sync();
+                    const uint32_t f = s_m[slot];
+                    m = 1u + (f < kLDThreads ? f : kLDThreads);
+                    trip++;
                 }
-#pragma unroll
-                for (uint32_t j = 0; j < kLDCand; j++)
-                    if (lane + 64u * j < m) hl[n + lane + 64u * j] = (uint16_t)(p + (lane + 64u * j) * L);
-                n += m;
-                p += m * L;
+                if (t == 0) {
+                    run_a[nr] = p | (d0.length << 16);
+                    run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
+                }
+                nr++;
+                nev += m;
+                if (d0.stop) {
+                    done = true;
+                    break;
+                }
+                p += m * (7u + d0.length);
             }
-            if (lane == 0) {
-                s_n = n;
-                s_bad = kLCNone;
-                if (!A.stash_pool) {
+            ld_sync();  // the pass's runs are in LDS
+            // ---- crc: one thread per OK record (none once the block has a failure:
+            // the records after it are dropped whatever their crc)
+            if (crc) {
+                for (uint32_t r = t; r < nev; r += kLDThreads) {
+                    uint32_t j = 0;  // the run holding event r: the last with first <= r
+                    for (uint32_t s = kLDRuns / 2; s; s >>= 1)
+                        if (j + s < nr && (run_b[j + s] & 0xffffu) <= r) j += s;
+                    const uint32_t ra = run_a[j], rb = run_b[j];
+                    if ((rb >> 24) != 1u) continue;
+                    const uint32_t len = ra >> 16;
+                    const uint32_t h = (ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len);
+                    const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
+                    const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+                    const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
+                    uint32_t d = dat[a];
+                    if (nd == 1u) d &= tmask;
+                    uint32_t x = ~d;
+                    if (hq) {
+                        const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
+                        x = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+                    }
+                    for (uint32_t k = 1; k + 1u < nd; k++) x = ld_z4(nt, lb, x, dat[a + k]);
+                    if (nd > 1u) x = ld_z4(nt, lb, x, dat[a + nd - 1u] & tmask);
+                    const uint32_t s = ld_z4(nt, lb, x);
+                    // s = z^(4 - tl)(state) when the last dword was padded: compare with
+                    // the stored crc's state shifted the same way
+                    uint32_t want = ~unmask_crc(lds32u(dat, h));
+                    for (uint32_t z = tl ? 4u - tl : 0u; z; z--) want = ld_z1(t0, want);
+                    if (s != want) atomicMin(&s_bad, h);
+                }
+            }
+            // ---- stash the pass's runs: one segment (+ a link slot when a pass follows)
+            if (t == 0) {
+                const uint64_t n = nr + (done ? 0u : 1u);
+                unsigned long long off = ~0ull;
+                if (!fit) {
+                } else if (!A.stash_pool) {
                     off = atomicAdd(A.stash_ctr, (unsigned long long)n);
-                } else {  // a fresh pool holds any block (kLDPool >= kLDMaxEv)
+                } else {  // a pass needs at most kLDRuns + 1 <= kLDPool entries
                     if (pool_hi - pool_lo < n) {
                         pool_lo = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
                         pool_hi = pool_lo + A.stash_pool;
@@ -853,75 +865,46 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     off = pool_lo;
                     pool_lo += n;
                 }
+                if (fit && off + n > A.stash_cap) {  // past the stash: the caller's event array is too small
+                    fit = false;
+                    off = ~0ull;
+                } else if (!fit) {
+                } else if (link != ~0ull) {
+                    A.stash[link] = (kLDLink << 56) | (n << 40) | off;
+                } else {
+                    seg0 = off | (n << 48);
+                }
+                link = done || !fit ? ~0ull : off + nr;
+                s_seg = off;
             }
-        }
-        LD_T(tw);
-        ld_sync();
-        LD_T(tc);
-        const uint32_t n = s_n;
-        if (A.checksum) {  // one thread per OK record: crc over type || payload (J/db/LogWriter.java:147)
-            for (uint32_t r = t; r < n; r += kLDThreads) {
-                const uint32_t h = hl[r];
-                const LCDecision d = lc_decide(blen - h, eof, lds32u(dat, h + 3u));
-                if (d.kind != 1u) continue;
-                const uint32_t x = ld_crc(T, dat, 0xffffffffu, h + 6u, h + 7u + d.length);
-                if (mask_crc(~x) != lds32u(dat, h)) atomicMin(&s_bad, r);
+            ld_sync();
+            const unsigned long long so = s_seg;
+            if (t < nr && so != ~0ull) {
+                const uint32_t first = run_b[t] & 0xffffu;
+                const uint32_t next = t + 1u < nr ? run_b[t + 1u] & 0xffffu : nev;
+                A.stash[so + t] = ld_run_entry(run_a[t], run_b[t], next - first);
             }
+            total += nev;
+            if (!done) ld_sync();  // the next pass's walk rewrites the runs
         }
         if (t == 0) {
-            s_off = off + n <= A.stash_cap ? off : ~0ull;  // past the stash: the caller's cap is short
-            A.count[b] = n;
-            A.dense_off[b] = s_off;
+            A.count[b] = total;
+            A.dense_off[b] = fit ? seg0 : ~0ull;
+            if (s_bad != kLCNone) A.first_bad[b] = s_bad;
         }
-        ld_sync();
-        LD_T(td);
-        // the events in file order (8 B each); the first failing record is BAD_CRC
-        // and the rest of the block is dropped (J/db/LogReader.java:359-367)
-        const uint32_t bad = s_bad;
-        const unsigned long long so = s_off;
-        if (so != ~0ull)
-            for (uint32_t r = t; r < n; r += kLDThreads) {
-                const uint32_t h = hl[r];
-                const LCDecision d = lc_decide(blen - h, eof, blen - h >= 7 ? lds32u(dat, h + 3u) : 0u);
-                const uint64_t kind = r == bad ? 2u : (bad != kLCNone && r > bad ? 0u : d.kind);
-                lc_st8(&A.stash[so + r], h | ((uint64_t)d.length << 16) | ((uint64_t)d.type << 32) | (kind << 40));
-            }
-#if JL_LD_PROF
-        LD_T(te);
-        acc[0] += tb - ta;
-        acc[1] += tw - tb2;
-        acc[6] += tc - tw;
-        acc[2] += td - tc;
-        acc[3] += te - td;
-        acc[4] += 1;
-        acc[5] += tb2 - tb;
-#endif
         b = bn;
     }
-#if JL_LD_PROF
-    if (t == 0)
-        for (int i = 0; i < 7; i++) atomicAdd(&g_ld_prof[i], (unsigned long long)acc[i]);
-#endif
 }
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + kLDSlice * 256 * kLDRep * 4 + JL_LD_HLCAP * 2 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + 8 * 16 * 32 * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
     hipLaunchKernelGGL(lc_dense_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);
     return hipGetLastError();
 }
-
-#if JL_LD_PROF
-// study builds: read (and clear) lc_dense's phase clocks [stage, walk, crc, stash, blocks, issue, walk barrier]
-extern "C" int jl_study_ld_prof(unsigned long long *out) {
-    static const unsigned long long zero[8] = {};
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ld_prof), sizeof(zero)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_ld_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
     hipLaunchKernelGGL(lc_walk_kernel, dim3((A.n_grp + 3) / 4), dim3(256), 0, st, A);

@@ -198,7 +198,10 @@ def test_jni_verify_log_vs_oracle(harness, oracle, tmp_path, mode, shape):
         cnt, grew = (int(x) for x in np.frombuffer(raw, "<u8", 2))
         got = np.frombuffer(raw, oracle.EVENT_DTYPE, cnt, 16)
         want = oracle.log_events(log, checksum=bool(checksum))
-        assert cnt == want.size
+        # the engine also reports the records a failure drops with the rest of its
+        # block (kind 0); the oracle's walk stops there: compare the live decisions
+        got = got[got["kind"] != 0]
+        assert got.size == want.size, checksum
         for f in ("offset", "length", "type", "kind"):
             assert np.array_equal(got[f], want[f]), (checksum, f)
         if checksum:
