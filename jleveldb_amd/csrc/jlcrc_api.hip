@@ -348,8 +348,11 @@ class CopyPool {
         }
         cv_.notify_all();
         run(j);  // the caller copies too, then waits for the pieces others took
+        // and for every worker to have left the job: j lives on this stack
         std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return j.left.load() == 0; });
+        done_.wait(lk, [&] { return j.left.load() == 0 && j.active == 0; });
+        auto it = std::find(q_.begin(), q_.end(), &j);
+        if (it != q_.end()) q_.erase(it);
     }
     ~CopyPool() {
         {
@@ -366,16 +369,14 @@ class CopyPool {
         const char *src;
         size_t n, pieces;
         std::atomic<size_t> next{0}, left{0};
+        int active = 0;  // pool workers inside run(): guarded by mu_
         Job(char *d, const char *s, size_t n_, size_t p) : dst(d), src(s), n(n_), pieces(p) { left = p; }
     };
     void run(Job &j) {  // copies pieces of j until none is left to take
         for (size_t i; (i = j.next.fetch_add(1)) < j.pieces;) {
             const size_t a = i * kPiece, b = std::min(j.n, a + kPiece);
             memcpy(j.dst + a, j.src + a, b - a);
-            if (j.left.fetch_sub(1) == 1) {
-                std::lock_guard<std::mutex> lk(mu_);
-                done_.notify_all();
-            }
+            j.left.fetch_sub(1);
         }
     }
     void work() {
@@ -388,9 +389,12 @@ class CopyPool {
                 q_.pop_front();
                 continue;
             }
+            j->active++;  // its caller returns only once this worker has left it
             lk.unlock();
-            run(*j);  // j outlives this: its caller waits until every piece is done
+            run(*j);
             lk.lock();
+            j->active--;
+            done_.notify_all();
         }
     }
     std::mutex mu_;
