@@ -621,21 +621,21 @@ __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // 
 __device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uint32_t c) {
     return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
 }
-// z^4(x) ^ w (x: the state XORed with the next 4 data bytes; z^4: 4 zero bytes)
-// from the nibble tables N_i[v] = z^4(v << 4i).  Layout: tables 2j and 2j + 1
-// share a 4 KiB block of 16 rows of 256 B, row v = 32 copies of N_2j[v] then 32
-// of N_2j+1[v]; lane l reads copy l mod 32, so every lookup of a wave hits 32
-// distinct banks.  The lookup address (v << 8 | half << 7 | 4 (l mod 32)) is one
-// v_perm_b32 of the nibbles spread one per byte (x & 0x0f0f0f0f, (x >> 4) & ...)
-// and lb (byte 0: 4 (l mod 32), byte 1: the same | 0x80): 11 VALU for 8 addresses.
-__device__ __forceinline__ uint32_t ld_z4(const uint32_t *nt, uint32_t lb, uint32_t x, uint32_t w = 0u) {
-    const uint32_t lo = x & 0x0f0f0f0fu, hi = (x >> 4) & 0x0f0f0f0fu;
+// z^(4k)(x) ^ w from the nibble tables of z^(4k) (k = 1..4: 4, 8, 12, 16 zero
+// bytes; x: a chain's state XORed with its latest data dword):
+//   z^(4k)(x) = XOR_i N_k,i[(x >> 4i) & 15],  N_k,i[v] = z^(4k)(v << 4i).
+// A 16-entry table fills 16 distinct LDS banks, so two lanes either read the
+// same entry (broadcast) or different banks: nibble lookups never conflict, with
+// ONE copy of each table (r3's byte tables, one copy beside the staged block,
+// spent 58 % of the LDS cycles in bank conflicts, profiles/r3n_pmc_lc_dense.json).
+// The lookup address is v_perm_b32 of the nibbles spread one per byte, x4.
+__device__ __forceinline__ uint32_t ld_zk(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
+    const uint32_t lo = (x << 2) & 0x3c3c3c3cu, hi = (x >> 2) & 0x3c3c3c3cu;
     uint32_t r[8];
 #pragma unroll
     for (uint32_t i = 0; i < 8; i++) {
-        const uint32_t sel = 0x0c0c0000u | ((i >> 1) << 8) | (4u + (i & 1u));
-        const uint32_t a = __builtin_amdgcn_perm(lb, i & 1u ? hi : lo, sel);
-        r[i] = *(const uint32_t *)((const char *)nt + 4096u * (i >> 1) + a);
+        const uint32_t a = __builtin_amdgcn_perm(0u, i & 1u ? hi : lo, 0x0c0c0c00u | (i >> 1));
+        r[i] = *(const uint32_t *)((const char *)tab + 64u * i + a);
     }
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], w));
 }
@@ -722,7 +722,7 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t nt[8 * 16 * 32];  // nibble tables N_i[v], 32 copies (bank = lane mod 32)
+    __shared__ uint32_t nt[4 * 128];      // nibble tables of z^4, z^8, z^12, z^16 (ld_zk)
     __shared__ uint32_t t0[256];
     __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
     __shared__ uint32_t run_b[kLDRuns];  // first event (of the pass) | type << 16 | kind << 24
@@ -733,19 +733,19 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
-    for (uint32_t w = t; w < 8u * 16u * 32u; w += kLDThreads) {  // N_i[v] = z^4(v << 4i), layout at ld_z4
-        const uint32_t i = 2u * (w >> 10) + ((w >> 5) & 1u), v = (w >> 6) & 15u;
+    for (uint32_t w = t; w < 4u * 128u; w += kLDThreads) {  // N_k,i[v] = z^(4k)(v << 4i) at 128 (k-1) + 16 i + v
+        const uint32_t k = (w >> 7) + 1u, i = (w >> 4) & 7u, v = w & 15u;
         uint32_t s = v << (4u * i);
-        for (int k = 0; k < 4; k++) s = ld_z1(t0, s);
+        for (uint32_t z = 0; z < 4u * k; z++) s = ld_z1(t0, s);
         nt[w] = s;
     }
     ld_sync();
-    const uint32_t lb = 4u * (lane & 31u) * 0x101u + 0x8000u;  // ld_z4's lane bytes
+    const uint32_t *N4 = nt, *N8 = nt + 128, *N12 = nt + 256, *N16 = nt + 384;
     // the first dword of a record whose crc range starts q & 3 = h bytes into a
     // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
     // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
     const uint32_t W0 = A.seed0;
-    const uint32_t C1 = ld_z4(nt, lb, W0 << 8), C2 = ld_z4(nt, lb, W0 << 16), C3 = ld_z4(nt, lb, W0 << 24);
+    const uint32_t C1 = ld_zk(N4, W0 << 8), C2 = ld_zk(N4, W0 << 16), C3 = ld_zk(N4, W0 << 24);
     LDSched sch;
     sch.init(A);
     uint64_t b = sch.next(A);
@@ -833,16 +833,32 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
                     const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
                     const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
+                    // the first dword, seeded (C_h folds in the seed dword before it)
                     uint32_t d = dat[a];
                     if (nd == 1u) d &= tmask;
-                    uint32_t x = ~d;
+                    uint32_t x0 = ~d;
                     if (hq) {
                         const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
-                        x = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+                        x0 = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
                     }
-                    for (uint32_t k = 1; k + 1u < nd; k++) x = ld_z4(nt, lb, x, dat[a + k]);
-                    if (nd > 1u) x = ld_z4(nt, lb, x, dat[a + nd - 1u] & tmask);
-                    const uint32_t s = ld_z4(nt, lb, x);
+                    // four chains: the record's dwords end-aligned on groups of 4 (o
+                    // zero dwords in front), chain c takes position c of every group
+                    // and steps z^16; at the end chain c still owes z^(16 - 4c)
+                    const uint32_t o = (4u - (nd & 3u)) & 3u, G = (nd + o) >> 2;
+                    const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
+                    uint32_t y[4];
+#pragma unroll
+                    for (uint32_t c = 0; c < 4; c++) y[c] = c < o ? 0u : (c == o ? x0 : D[c]);
+                    if (G == 1u && o < 3u) y[3] &= tmask;
+                    for (uint32_t g = 1; g < G; g++) {
+                        uint32_t v[4];
+#pragma unroll
+                        for (uint32_t c = 0; c < 4; c++) v[c] = D[4u * g + c];
+                        if (g + 1u == G) v[3] &= tmask;
+#pragma unroll
+                        for (uint32_t c = 0; c < 4; c++) y[c] = ld_zk(N16, y[c], v[c]);
+                    }
+                    const uint32_t s = ld_zk(N16, y[0]) ^ ld_zk(N12, y[1]) ^ ld_zk(N8, y[2]) ^ ld_zk(N4, y[3]);
                     // s = z^(4 - tl)(state) when the last dword was padded: compare with
                     // the stored crc's state shifted the same way
                     uint32_t want = ~unmask_crc(lds32u(dat, h));
@@ -898,7 +914,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + 8 * 16 * 32 * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * 128 * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
