@@ -1,0 +1,115 @@
+// copy_pool.hpp — persistent host threads for the staging copies of the
+// host-memory entry points (jlcrc_api.hip par_memcpy); header-only so the CPU
+// tests can drive it under ThreadSanitizer (tests/cpp/copy_pool_test.cpp).
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstddef>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace jlhost {
+
+// Persistent staging workers for pageable -> pinned copies (one core copies at
+// ~10-20 GB/s, well under PCIe's ~55): a copy is cut into one piece per thread
+// (at least 256 KiB) that the caller and up to JL_OPT_STAGE_THREADS - 1 pool
+// threads take from a shared cursor.  Persistent threads, because starting
+// threads per call (r3) cost more than a one-table copy itself, so r3 copied
+// anything under 4 MiB on one core.  Idle workers spin for kSpinUs before they
+// sleep, so back-to-back calls do not pay a futex wake-up per copy.  Concurrent
+// callers queue their copies; every caller also works on its own.
+class CopyPool {
+  public:
+    static constexpr size_t kMinPiece = 256u << 10;
+    static constexpr double kSpinUs = 300.0;
+    void copy(void *dst, const void *src, size_t n, int threads) {
+        if (n < 2 * kMinPiece || threads <= 1) {
+            memcpy(dst, src, n);
+            return;
+        }
+        const size_t piece = std::max<size_t>(kMinPiece, ((n + threads - 1) / threads + 4095) & ~(size_t)4095);
+        Job j{(char *)dst, (const char *)src, n, piece};
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            while ((int)th_.size() < threads - 1 && (int)th_.size() < 63) th_.emplace_back([this] { work(); });
+            q_.push_back(&j);
+            queued_.fetch_add(1);
+        }
+        cv_.notify_all();
+        run(j);  // the caller copies too, then waits for the pieces others took
+        // and for every worker to have left the job: j lives on this stack
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return j.left.load() == 0 && j.active == 0; });
+        auto it = std::find(q_.begin(), q_.end(), &j);
+        if (it != q_.end()) {
+            q_.erase(it);
+            queued_.fetch_sub(1);
+        }
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+
+  private:
+    struct Job {
+        char *dst;
+        const char *src;
+        size_t n, piece, pieces;
+        std::atomic<size_t> next{0}, left{0};
+        int active = 0;  // pool workers inside run(): guarded by mu_
+        Job(char *d, const char *s, size_t n_, size_t pc) : dst(d), src(s), n(n_), piece(pc), pieces((n_ + pc - 1) / pc) {
+            left = pieces;
+        }
+    };
+    void run(Job &j) {  // copies pieces of j until none is left to take
+        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces;) {
+            const size_t a = i * j.piece, b = std::min(j.n, a + j.piece);
+            memcpy(j.dst + a, j.src + a, b - a);
+            j.left.fetch_sub(1);
+        }
+    }
+    void work() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            if (q_.empty() && !stop_) {  // spin a while (unlocked) before sleeping
+                lk.unlock();
+                const auto t0 = std::chrono::steady_clock::now();
+                while (queued_.load() == 0 &&
+                       std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < kSpinUs)
+                    __builtin_ia32_pause();
+                lk.lock();
+            }
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            if (stop_) return;
+            Job *j = q_.front();
+            if (j->next.load() >= j->pieces) {  // every piece taken: the job leaves the queue
+                q_.pop_front();
+                queued_.fetch_sub(1);
+                continue;
+            }
+            j->active++;  // its caller returns only once this worker has left it
+            lk.unlock();
+            run(*j);
+            lk.lock();
+            j->active--;
+            done_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::deque<Job *> q_;
+    std::atomic<int> queued_{0};  // jobs in q_ (read by spinning workers without the lock)
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
+}  // namespace jlhost

@@ -142,6 +142,20 @@ constexpr uint32_t kLCMB = 16384, kLCSelB = 30720;
 #define JL_RING_SLACK 2
 #endif
 
+// Study builds (tools/build_study.sh ... -DJL_GV4_WAVETIME=1): every wave's start
+// and end time (s_memrealtime, 100 MHz, one clock for the whole chip), read with
+// jl_study_gv4_wavetime_m<mode> (tools/gv4_wavetime.py): how long the last waves
+// run after the others have finished (the grid's tail).
+#ifndef JL_GV4_WAVETIME
+#define JL_GV4_WAVETIME 0
+#endif
+#if JL_GV4_WAVETIME
+#define JL_WT_CAT2(a, b) a##b
+#define JL_WT_CAT(a, b) JL_WT_CAT2(a, b)
+#define JL_WT_ARR JL_WT_CAT(g_gv4_wt_m, JL_MODE)
+__device__ unsigned long long JL_WT_ARR[2 * 16384];
+#endif
+
 template <int MODE>
 struct GV4 {
     static constexpr bool VERIFY = MODE == MODE_TABLE_VERIFY || MODE == MODE_LOG_VERIFY;
@@ -435,6 +449,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint32_t bx = (G & 7u) ? b : (b & 7u) * (G >> 3) + (b >> 3);
     const uint32_t w = uni((threadIdx.x >> 6) * G + bx);
+#if JL_GV4_WAVETIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t R = A.desc ? *A.n_rounds : (uint32_t)((A.P.n + 7u) / 8u);  // rounds < 2^31
     // compute cursor: the wave's first round with K > 0
     uint32_t ci = 0, cr = uni(gv4_deal(0u, w, waves, R));
@@ -735,9 +752,24 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
 #undef JL_LOAD
 #undef JL_GLD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring drains before the wave ends
+#if JL_GV4_WAVETIME
+    if (lane == 0 && w < 16384u) {
+        JL_WT_ARR[2u * w] = wt0;
+        JL_WT_ARR[2u * w + 1u] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 }  // namespace jlk
+
+#if JL_GV4_WAVETIME
+// study builds: per wave [start, end] of the last crc_gv4_kernel launch of this mode (and clear them)
+extern "C" int JL_WT_CAT(jl_study_gv4_wavetime_m, JL_MODE)(unsigned long long *out) {
+    static unsigned long long zero[2 * 16384];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jlk::JL_WT_ARR), sizeof(zero)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(jlk::JL_WT_ARR), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace jlk {
 

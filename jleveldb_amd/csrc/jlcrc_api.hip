@@ -17,6 +17,7 @@
 
 #include "../../include/jlcrc.h"
 #include "crc_math.hpp"
+#include "copy_pool.hpp"
 #include "host_paths.hpp"
 #include "jlcrc_kernels.hpp"
 
@@ -326,85 +327,8 @@ struct HostSrc {
     }
 };
 
-// Persistent staging workers for pageable -> pinned copies (one core copies at
-// ~10-20 GB/s, well under PCIe's ~55): a copy is cut into 256 KiB pieces that
-// the caller and up to JL_OPT_STAGE_THREADS - 1 pool threads take from a shared
-// cursor.  Persistent threads, because starting threads per call (r3) cost more
-// than a one-table copy itself, so r3 copied anything under 4 MiB on one core.
-// Concurrent callers queue their copies; every caller also works on its own.
-class CopyPool {
-  public:
-    static constexpr size_t kPiece = 256u << 10;
-    void copy(void *dst, const void *src, size_t n, int threads) {
-        if (n < 2 * kPiece || threads <= 1) {
-            memcpy(dst, src, n);
-            return;
-        }
-        Job j{(char *)dst, (const char *)src, n, (n + kPiece - 1) / kPiece};
-        {
-            std::unique_lock<std::mutex> lk(mu_);
-            while ((int)th_.size() < threads - 1 && (int)th_.size() < 63) th_.emplace_back([this] { work(); });
-            q_.push_back(&j);
-        }
-        cv_.notify_all();
-        run(j);  // the caller copies too, then waits for the pieces others took
-        // and for every worker to have left the job: j lives on this stack
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return j.left.load() == 0 && j.active == 0; });
-        auto it = std::find(q_.begin(), q_.end(), &j);
-        if (it != q_.end()) q_.erase(it);
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : th_) t.join();
-    }
-
-  private:
-    struct Job {
-        char *dst;
-        const char *src;
-        size_t n, pieces;
-        std::atomic<size_t> next{0}, left{0};
-        int active = 0;  // pool workers inside run(): guarded by mu_
-        Job(char *d, const char *s, size_t n_, size_t p) : dst(d), src(s), n(n_), pieces(p) { left = p; }
-    };
-    void run(Job &j) {  // copies pieces of j until none is left to take
-        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces;) {
-            const size_t a = i * kPiece, b = std::min(j.n, a + kPiece);
-            memcpy(j.dst + a, j.src + a, b - a);
-            j.left.fetch_sub(1);
-        }
-    }
-    void work() {
-        std::unique_lock<std::mutex> lk(mu_);
-        for (;;) {
-            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-            if (stop_) return;
-            Job *j = q_.front();
-            if (j->next.load() >= j->pieces) {  // every piece taken: the job leaves the queue
-                q_.pop_front();
-                continue;
-            }
-            j->active++;  // its caller returns only once this worker has left it
-            lk.unlock();
-            run(*j);
-            lk.lock();
-            j->active--;
-            done_.notify_all();
-        }
-    }
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    std::deque<Job *> q_;
-    std::vector<std::thread> th_;
-    bool stop_ = false;
-};
-CopyPool &copy_pool() {
-    static CopyPool *p = new CopyPool;  // never destroyed: workers may outlive static destruction order
+jlhost::CopyPool &copy_pool() {
+    static jlhost::CopyPool *p = new jlhost::CopyPool;  // never destroyed: workers may outlive static destruction order
     return *p;
 }
 void par_memcpy(void *dst, const void *src, size_t n) { copy_pool().copy(dst, src, n, std::max(1, opt().stage_threads)); }
@@ -415,7 +339,7 @@ void par_memcpy(void *dst, const void *src, size_t n) { copy_pool().copy(dst, sr
 // A pageable source is staged in pieces of kStagePiece, each DMA'd as soon as it
 // is in pinned memory, so the copy engine works on piece i while the host copies
 // piece i + 1 (one call's latency is then about the host copy, not copy + DMA).
-constexpr uint64_t kStagePiece = 1ull << 20;
+constexpr uint64_t kStagePiece = 4ull << 20;
 int slot_put_data(Slot &sl, const HostSrc &src, uint64_t off, uint64_t bytes) {
     JL_HIP(hipStreamWaitEvent(sl.st, sl.used, 0));
     const uint8_t *p = src.p + off;

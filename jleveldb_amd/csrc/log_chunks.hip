@@ -432,16 +432,19 @@ __device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
 // then writes their events 64 at a time, lane = event, each finding its run by
 // a binary search over the lanes' prefixes.  Event k of a run: header at offset
 // + k (7 + length).
-__device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint64_t ev0, uint64_t doff) {
+__device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint64_t ev0, uint64_t doff, uint64_t e0) {
     const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     uint64_t so = doff & 0xffffffffffffull;
     uint32_t n = (uint32_t)(doff >> 48);
     uint64_t k0 = 0;  // events of the block written so far
+    bool first = true;
     while (n) {
         uint32_t nn = 0;  // the next segment (a link in this one's last entry)
         uint64_t sn = 0;
         for (uint32_t r0 = 0; r0 < n; r0 += 64u) {
-            const uint64_t e = r0 + lane < n ? lc_ld8(&A.stash[so + r0 + lane]) : 0ull;
+            // the first segment's first 64 entries came with the block's other loads (e0)
+            const uint64_t e = r0 + lane < n ? (first ? e0 : lc_ld8(&A.stash[so + r0 + lane])) : 0ull;
+            first = false;
             const bool link = r0 + lane < n && (e >> 56) == kLDLinkKind;
             const uint64_t lb = __builtin_amdgcn_ballot_w64(link);
             if (lb) {
@@ -496,26 +499,32 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
     // the wave's blocks wv, wv + 16, ... of the group: all their loads first
     constexpr uint32_t kPer = kLCGroup / kLCBuildWaves;
     uint32_t cnt[kPer];
-    uint64_t st[kPer], sl[kPer];
+    uint64_t st[kPer], sl[kPer], doff[kPer];
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         cnt[i] = b < A.n_blocks ? A.count[b] : 0u;  // dense blocks: counted by lc_dense
         st[i] = b < A.n_blocks ? A.start[b] : 0u;
+        doff[i] = b < A.n_blocks ? A.dense_off[b] : kLCNotDense;
     }
+    // a block's walk slots, or a dense block's first 64 stash entries (its runs)
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
-        sl[i] = lane < cnt[i] && cnt[i] <= kLCSlots ? A.slots[b * kLCSlots + lane] : 0ull;
+        if (doff[i] == kLCNotDense) {
+            sl[i] = lane < cnt[i] && cnt[i] <= kLCSlots ? A.slots[b * kLCSlots + lane] : 0ull;
+        } else {
+            const uint32_t n0 = doff[i] == ~0ull ? 0u : (uint32_t)(doff[i] >> 48);
+            sl[i] = lane < n0 ? lc_ld8(&A.stash[(doff[i] & 0xffffffffffffull) + lane]) : 0ull;
+        }
     }
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         if (b >= A.n_blocks) break;
-        const uint64_t doff = A.dense_off[b];
-        if (doff != kLCNotDense) {  // dense block: its events expanded from lc_dense's runs
-            if (doff == ~0ull) continue;  // did not fit: the event array is too small anyway
-            lc_expand_runs(A, b, st[i], doff);
+        if (doff[i] != kLCNotDense) {  // dense block: its events expanded from lc_dense's runs
+            if (doff[i] == ~0ull) continue;  // did not fit: the event array is too small anyway
+            lc_expand_runs(A, b, st[i], doff[i], sl[i]);
             continue;
         }
         const uint64_t bs = b * 32768u, s = sl[i];
