@@ -289,25 +289,34 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 }
 
 
-// Round dealing: the i-th round of wave w (of W) is w + iW, or kGvNoRound past
-// its last.  The table is sorted by K ascending; heavy-first orders (descending,
-// or descending in snake passes, which balance the waves' step totals to ~1 %
-// instead of ~9 % on C3) measured 1-2 % slower on C3 (r2 A/B), ascending snake
-// passes no faster.
+// Round dealing (r4): workgroup b (XCD-major index bx of G) owns the rounds
+// j G + bx, j = 0, 1, ...; its 16 waves take them one at a time from a counter
+// in LDS, in ascending j, so a wave that runs faster takes more rounds.  r3 dealt
+// them statically (round i W + w to wave w) and every wave had the same work,
+// but the 4 waves of a SIMD do not run at the same rate — issue goes to the
+// oldest first — so on C3 the waves of slots 0-3 finished at ~1.0 ms, slots
+// 4-7 at ~1.3, 8-11 at ~1.7 and 12-15 at ~1.9 ms, and the kernel ran its last
+// ~0.8 ms with ever fewer loads in flight (tools/gv4_wavetime.py,
+// profiles/r4i_gv4_wavetime.json).  The taken rounds go through a 16-entry
+// queue per wave in LDS: the prefetch cursor takes round i (and i + 1, whose
+// descriptor it prefetches) from the counter, the compute cursor, up to P
+// entries behind, reads the same sequence back.  The table is sorted by K
+// ascending and j ascends, so a wave's K never decreases (desc_issue relies on
+// that).  The counter and queues sit in dwords [kGvDynDword, +257) of the LDS
+// image, unused by both gv4 images (zero when the image is loaded).
 constexpr uint32_t kGvNoRound = 0xffffffffu;  // >= any round count (< 2^31)
-__device__ __forceinline__ uint32_t gv4_deal(uint32_t i, uint32_t w, uint32_t W, uint32_t R) {
-    const uint64_t x = (uint64_t)i * W + w;
-    return x < R ? (uint32_t)x : kGvNoRound;
-}
+constexpr uint32_t kGvDynDword = 7935;       // [0] the workgroup's counter, then 16 queues of 16 rounds
 
-// Prefetch cursor: walks the wave's rounds gv4_deal(i, w, ...) entry by entry.
+// Prefetch cursor: walks the wave's rounds (seq(i), from the workgroup's counter) entry by entry.
 // L2W (study variant 7): every round's bytes are read from a 1 MiB window at the
 // start of the arena instead (the same round table and addressing pattern, the
 // data L2-resident: the CRC math without the HBM stream).
 template <int MODE, bool DBG, bool L2W = false>
 struct GPF {
-    uint32_t r, R, W;  // rounds (< 2^31)
-    uint32_t i, w;     // r = gv4_deal(i, w, W, R)
+    uint32_t r, R, G, bx;  // rounds (< 2^31); the workgroup's rounds are j G + bx
+    uint32_t i;            // r = seq(i)
+    uint32_t made;         // rounds taken into the queue so far (seq(i) for i < made is known)
+    uint32_t *ctr, *Q;     // LDS: the workgroup's counter, this wave's queue
     uint32_t e, E, K;
     uint32_t k;      // sequence number of the current round (descriptor set k & 1)
     bool vec_next;   // the next round's descriptor was issued into set (k+1) & 1
@@ -316,6 +325,19 @@ struct GPF {
     uint64_t side_addr;   // per lane: the side chunk
     uint64_t dummy;       // a mapped address (zero page) for lanes with nothing to load
 
+    // the wave's i-th round: taken from the workgroup's counter the first time it
+    // is asked for (i == made), read back from the queue after that
+    __device__ __forceinline__ uint32_t seq(uint32_t i_) {
+        if (i_ < made) return uni(Q[i_ & 15u]);
+        uint32_t j = 0;
+        if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u) j = atomicAdd(ctr, 1u);
+        j = uni(j);
+        const uint64_t x = (uint64_t)j * G + bx;
+        const uint32_t rr = x < R ? (uint32_t)x : kGvNoRound;
+        Q[made & 15u] = rr;  // every lane writes the same value
+        made++;
+        return rr;
+    }
     __device__ __forceinline__ void setup(const GV4Args &A, uint32_t lane, bool vec) {
         const uint32_t q = lane >> 3, l = lane & 7u;  // group, lane in group
         RoundView v;
@@ -326,7 +348,7 @@ struct GPF {
                 v = round_view<MODE>(A, r, q);
                 if (uni(v.K) != 0u) break;
                 i++;
-                r = uni(gv4_deal(i, w, W, R));
+                r = seq(i);
                 if (r >= R) return;
             }
         }
@@ -339,7 +361,7 @@ struct GPF {
         //  * E_{k-1} >= P: the compute cursor has already read round k-1's
         //    descriptor from that set (it is P entries behind)
         // gv4 finish() takes the same decision from the same E values
-        const uint32_t rn = uni(gv4_deal(i + 1u, w, W, R));
+        const uint32_t rn = seq(i + 1u);
         vec_next = A.desc && E > (uint32_t)JL_GV4_RING && (k == 0u || Eprev >= (uint32_t)JL_GV4_RING) && rn < R;
         if (vec_next) desc_issue(A, rn, q, (k + 1u) & 1u);
         uint64_t p = v.p;
@@ -367,13 +389,16 @@ struct GPF {
         side_addr = l == 0u ? c0 : (l == 1u ? c1 : dummy);
         e = 0;
     }
-    __device__ __forceinline__ void init(const GV4Args &A, uint32_t i0, uint32_t w0, uint32_t waves, uint32_t nr,
+    __device__ __forceinline__ void init(const GV4Args &A, uint32_t *lds, uint32_t g, uint32_t b, uint32_t nr,
                                          uint32_t lane, uint64_t dmy) {
-        i = i0;
-        w = w0;
-        r = gv4_deal(i0, w0, waves, nr);
-        W = waves;
+        ctr = lds + kGvDynDword;
+        Q = lds + kGvDynDword + 1u + 16u * (threadIdx.x >> 6);
+        made = 0;
+        G = g;
+        bx = b;
         R = nr;
+        i = 0;
+        r = seq(0);
         dummy = dmy;
         k = 0;
         E = 0;
@@ -413,7 +438,7 @@ struct GPF {
         }
         if (++e == E) {
             i++;
-            r = gv4_deal(i, w, W, R);
+            r = seq(i);
             k++;
             if (r < R) setup(A, lane, vec_next);
             r = uni(r);
@@ -442,33 +467,29 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     const uint32_t lane = threadIdx.x & 63u, q = lane >> 3, l = lane & 7u;
     const GLanes gl(lane);
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    // Wave ids run across workgroups first: consecutive rounds go to neighbouring
-    // CUs of one XCD (workgroup b runs on XCD b % 8), so the run of heavy rounds
-    // at the end of the K-sorted table spreads over every CU (C3 2.19 -> 2.13 ms;
-    // blockIdx-major ids put them all on the first ~60 CUs)
+    // Workgroup ids XCD-major (workgroup b runs on XCD b % 8): consecutive rounds
+    // go to neighbouring CUs of one XCD, so the run of heavy rounds at the end of
+    // the K-sorted table spreads over every CU (r2: C3 2.19 -> 2.13 ms; with
+    // blockIdx-major ids they all landed on the first ~60 CUs)
     const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint32_t bx = (G & 7u) ? b : (b & 7u) * (G >> 3) + (b >> 3);
-    const uint32_t w = uni((threadIdx.x >> 6) * G + bx);
 #if JL_GV4_WAVETIME
+    const uint32_t w = uni((threadIdx.x >> 6) * G + bx);
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const uint32_t R = A.desc ? *A.n_rounds : (uint32_t)((A.P.n + 7u) / 8u);  // rounds < 2^31
-    // compute cursor: the wave's first round with K > 0
-    uint32_t ci = 0, cr = uni(gv4_deal(0u, w, waves, R));
-    RoundView cv;
-    for (;;) {
-        if (cr >= R) return;
-        cv = round_view<MODE>(A, cr, q);
-        if (uni(cv.K) != 0u) break;
-        ci++;
-        cr = uni(gv4_deal(ci, w, waves, R));
-    }
+    (void)waves;
+    // the prefetch cursor takes the wave's first round with K > 0 (round dealing
+    // above); the compute cursor starts on the same one
+    GPF<MODE, DBG, VAR == 7> pf;
+    pf.init(A, lds, G, bx, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
+    if (pf.r >= R) return;  // the workgroup's rounds are all taken: no ring started
+    uint32_t ci = pf.i, cr = pf.r;
+    RoundView cv = round_view<MODE>(A, cr, q);
     const uint32_t e0 = GV4<MODE>::side(A) ? 1u : 0u;
     uint32_t zero_v;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
 
-    GPF<MODE, DBG, VAR == 7> pf;
-    pf.init(A, ci, w, waves, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
     // The ring lives in PINNED registers (JL_GV4_SLOTS, the two prefetched
     // round-descriptor sets JL_GV4_DQ0/1 just below it), above what the
     // compiler allocates: the register allocator
@@ -641,13 +662,13 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         ck++;
         if (vec) {
             ci++;
-            cr = uni(gv4_deal(ci, w, waves, R));
+            cr = pf.seq(ci);
             if (cr >= R) return false;
             cv = desc_read<MODE>(A, ck & 1u);
         } else {
             for (;;) {
                 ci++;
-                cr = uni(gv4_deal(ci, w, waves, R));
+                cr = pf.seq(ci);
                 if (cr >= R) return false;
                 cv = round_view<MODE>(A, cr, q);
                 if (uni(cv.K) != 0u) break;

@@ -729,6 +729,20 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
     return (uint64_t)ra | ((uint64_t)cnt << 32) | ((uint64_t)(rb >> 16) << 48);
 }
 
+// Study builds (-DJL_LD_PROF=1, tools/ld_prof.py): per workgroup, shader clocks
+// (s_memtime of thread 0) spent in each phase over all its blocks — [0] waiting
+// for / storing the staged block, [1] walk, [2] crc, [3] stash, [4] blocks —
+// and its start / end time (s_memrealtime, 100 MHz, one clock for the chip).
+#ifndef JL_LD_PROF
+#define JL_LD_PROF 0
+#endif
+#if JL_LD_PROF
+__device__ unsigned long long g_ld_prof[4096 * 8];
+#define LD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define LD_T(v)
+#endif
+
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
     __shared__ uint32_t nt[4 * 128];      // nibble tables of z^4, z^8, z^12, z^16 (ld_zk)
@@ -762,7 +776,12 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
     uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
+#if JL_LD_PROF
+    uint64_t acc[5] = {0, 0, 0, 0, 0};
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     while (b < A.n_blocks) {
+        LD_T(ta);
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
@@ -783,6 +802,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         ld_sync();
         const uint64_t bn = sch.next(A);  // its bytes load during this block's work
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
+        LD_T(tb);
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
         uint64_t seg0 = ~0ull;      // thread 0: the block's first segment (stash offset | entries << 48)
         uint64_t link = ~0ull;      // thread 0: the previous segment's link slot
@@ -828,6 +848,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 p += m * (7u + d0.length);
             }
             ld_sync();  // the pass's runs are in LDS
+            LD_T(tc);
             // ---- crc: one thread per OK record (none once the block has a failure:
             // the records after it are dropped whatever their crc)
             if (crc) {
@@ -875,6 +896,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     if (s != want) atomicMin(&s_bad, h);
                 }
             }
+            LD_T(td);
             // ---- stash the pass's runs: one segment (+ a link slot when a pass follows)
             if (t == 0) {
                 const uint64_t n = nr + (done ? 0u : 1u);
@@ -911,7 +933,17 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
             total += nev;
             if (!done) ld_sync();  // the next pass's walk rewrites the runs
+#if JL_LD_PROF
+            LD_T(te);
+            acc[1] += tc - tb;
+            acc[2] += td - tc;
+            acc[3] += te - td;
+#endif
         }
+#if JL_LD_PROF
+        acc[0] += tb - ta;
+        acc[4] += 1;
+#endif
         if (t == 0) {
             A.count[b] = total;
             A.dense_off[b] = fit ? seg0 : ~0ull;
@@ -919,7 +951,23 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         b = bn;
     }
+#if JL_LD_PROF
+    if (t == 0 && blockIdx.x < 4096u) {
+        for (int i = 0; i < 5; i++) g_ld_prof[8u * blockIdx.x + i] = acc[i];
+        g_ld_prof[8u * blockIdx.x + 5] = rt0;
+        g_ld_prof[8u * blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
+
+#if JL_LD_PROF
+// study builds: read (and clear) lc_dense's per-workgroup phase clocks (see g_ld_prof)
+extern "C" int jl_study_ld_prof(unsigned long long *out) {
+    static unsigned long long zero[4096 * 8];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ld_prof), sizeof(zero)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ld_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {

@@ -28,6 +28,7 @@ def read(mode):
     fn.argtypes = [ctypes.c_void_p]
     assert fn(buf.ctypes.data) == 0
     t = buf.reshape(-1, 2)
+    np.save(os.path.join("gpurun_out", f"wavetime_m{mode}_{len(os.listdir('gpurun_out')) if os.path.isdir('gpurun_out') else 0}.npy"), t)
     t = t[t[:, 1] > 0].astype(np.float64) / 100.0  # us
     t0 = t[:, 0].min()
     end = t[:, 1] - t0
