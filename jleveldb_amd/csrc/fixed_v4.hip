@@ -42,7 +42,17 @@
 #define JL_RING_SLACK 2  // see general_v4.hip
 #endif
 
+// Study builds (-DJL_GV4_WAVETIME=1, tools/gv4_wavetime.py): every wave's start
+// and end time (s_memrealtime), read with jl_study_fx_wavetime.
+#ifndef JL_GV4_WAVETIME
+#define JL_GV4_WAVETIME 0
+#endif
+
 namespace jlk {
+
+#if JL_GV4_WAVETIME
+__device__ unsigned long long g_fx_wt[2 * 16384];
+#endif
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
@@ -147,6 +157,10 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave);  // group of 64 blocks
     if (g * 64u >= n_blocks) return;
+#if JL_GV4_WAVETIME
+    const uint64_t wid = g;
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint32_t *slot = lds + kV4SlotDword + wave * 64u;
     const uint64_t dbase = (uint64_t)(uintptr_t)data;
     const uint32_t do_mask = flags & 1u;
@@ -196,6 +210,12 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (zero-range) loads
+#if JL_GV4_WAVETIME
+    if (lane == 0 && wid < 16384u) {
+        g_fx_wt[2u * wid] = wt0;
+        g_fx_wt[2u * wid + 1u] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
@@ -209,3 +229,12 @@ hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_bl
 }
 
 }  // namespace jlk
+
+#if JL_GV4_WAVETIME
+// study builds: per wave [start, end] of the last crc_fixed4k_v4_kernel launch (and clear them)
+extern "C" int jl_study_fx_wavetime(unsigned long long *out) {
+    static unsigned long long zero[2 * 16384];
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jlk::g_fx_wt), sizeof(zero)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(jlk::g_fx_wt), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -290,20 +290,22 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 
 
 // Round dealing (r4): workgroup b (XCD-major index bx of G) owns the rounds
-// j G + bx, j = 0, 1, ...; its 16 waves take them one at a time from a counter
-// in LDS, in ascending j, so a wave that runs faster takes more rounds.  r3 dealt
-// them statically (round i W + w to wave w) and every wave had the same work,
-// but the 4 waves of a SIMD do not run at the same rate — issue goes to the
-// oldest first — so on C3 the waves of slots 0-3 finished at ~1.0 ms, slots
-// 4-7 at ~1.3, 8-11 at ~1.7 and 12-15 at ~1.9 ms, and the kernel ran its last
-// ~0.8 ms with ever fewer loads in flight (tools/gv4_wavetime.py,
-// profiles/r4i_gv4_wavetime.json).  The taken rounds go through a 16-entry
-// queue per wave in LDS: the prefetch cursor takes round i (and i + 1, whose
-// descriptor it prefetches) from the counter, the compute cursor, up to P
-// entries behind, reads the same sequence back.  The table is sorted by K
-// ascending and j ascends, so a wave's K never decreases (desc_issue relies on
-// that).  The counter and queues sit in dwords [kGvDynDword, +257) of the LDS
-// image, unused by both gv4 images (zero when the image is loaded).
+// R - 1 - (j G + bx), j = 0, 1, ... — the table is sorted by K ascending, so
+// heaviest first — and its 16 waves take them one at a time from a counter in
+// LDS: a wave that runs faster takes more rounds, and the rounds left at the end
+// are the lightest.  r3 dealt them statically in ascending K (round i W + w to
+// wave w) and every wave had the same work, but the 4 waves of a SIMD do not run
+// at the same rate — issue goes to the oldest first — so on C3 the waves of
+// slots 0-3 finished at ~1.0 ms, slots 4-7 at ~1.3, 8-11 at ~1.7 and 12-15 at
+// ~1.9 ms, and the kernel ran its last ~0.8 ms with ever fewer loads in flight
+// (tools/gv4_wavetime.py, profiles/r4i_gv4_wavetime.json); dealt dynamically but
+// still ascending, C3's heaviest rounds (8 blocks of 64 KiB, ~0.3 ms for one
+// wave) came last and left a 0.4 ms tail (r4j).  The taken rounds go through a
+// 16-entry queue per wave in LDS: the prefetch cursor takes round i (and i + 1,
+// whose descriptor it prefetches) from the counter, the compute cursor, up to P
+// entries behind, reads the same sequence back.  The counter and queues sit in
+// dwords [kGvDynDword, +257) of the LDS image, unused by both gv4 images (zero
+// when the image is loaded).
 constexpr uint32_t kGvNoRound = 0xffffffffu;  // >= any round count (< 2^31)
 constexpr uint32_t kGvDynDword = 7935;       // [0] the workgroup's counter, then 16 queues of 16 rounds
 
@@ -333,7 +335,7 @@ struct GPF {
         if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u) j = atomicAdd(ctr, 1u);
         j = uni(j);
         const uint64_t x = (uint64_t)j * G + bx;
-        const uint32_t rr = x < R ? (uint32_t)x : kGvNoRound;
+        const uint32_t rr = x < R ? R - 1u - (uint32_t)x : kGvNoRound;  // heaviest first
         Q[made & 15u] = rr;  // every lane writes the same value
         made++;
         return rr;

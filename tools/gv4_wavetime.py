@@ -24,7 +24,7 @@ L = jl.lib()
 
 def read(mode):
     buf = np.zeros(2 * 16384, np.uint64)
-    fn = getattr(L, f"jl_study_gv4_wavetime_m{mode}")
+    fn = getattr(L, f"jl_study_gv4_wavetime_m{mode}" if mode != "fx" else "jl_study_fx_wavetime")
     fn.argtypes = [ctypes.c_void_p]
     assert fn(buf.ctypes.data) == 0
     t = buf.reshape(-1, 2)
@@ -38,6 +38,18 @@ def read(mode):
 
 
 dev = torch.device("cuda:0")
+c2 = torch.empty(1 << 32, dtype=torch.uint8, device=dev)
+jl.fill_random_dev(c2, wl.SEED)
+out = torch.empty(1 << 20, dtype=torch.int32, device=dev)
+for _ in range(20):
+    jl.crc32c_fixed_dev(c2, 4096, out=out)
+torch.cuda.synchronize()
+read("fx")
+jl.crc32c_fixed_dev(c2, 4096, out=out)
+torch.cuda.synchronize()
+print(json.dumps({"C2 crc_fixed4k_v4_kernel": read("fx")}), flush=True)
+del c2
+torch.cuda.empty_cache()
 lens = wl.c3_lengths()
 offs = wl.packed_offsets(lens)
 total = int(offs[-1]) + int(lens[-1])
