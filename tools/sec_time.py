@@ -26,7 +26,8 @@ if which == "all" or "c3" in which.split(","):
     torch.cuda.empty_cache()
 if which in ("all", "dispatch"):
     print(json.dumps(bench.dispatch_latency()), flush=True)
-sets = wl.C5_SETS if which in ("all", "c5") else [x for x in which.split(",") if x in wl.C5_SETS]
+ws = which.split(",")
+sets = wl.C5_SETS if which == "all" or "c5" in ws else [x for x in ws if x in wl.C5_SETS]
 for s in sets:
     r = bench.secondary_c5(dev, stream, steps, 3, which=s, cpu=False, host_copy=False)
     print(json.dumps({k: r[k] for k in ("config", "GiB_per_s", "achieved_GBps", "achieved_frac_of_peak", "ms_per_step",
