@@ -145,6 +145,10 @@ struct V4Wave {
     }
 };
 
+#ifndef JL_FX_DYN
+#define JL_FX_DYN 0  // study: rounds dealt from an LDS counter (below); r4 A/B in DESIGN.md
+#endif
+#if JL_FX_DYN
 // Rounds (R blocks each) are dealt inside each workgroup from a counter in LDS
 // (r4): workgroup b owns rounds j G + b, j = 0, 1, ..., and each of its waves
 // takes the next j when it starts a round's prefetch, so a wave that runs faster
@@ -221,6 +225,82 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
     }
 #endif
 }
+
+#else
+template <int LPB, bool NT, int RING = 16, int THREADS = 1024>
+__global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__restrict__ img,
+                                                                 const uint8_t *__restrict__ data, uint64_t n_blocks,
+                                                                 uint32_t flags, uint32_t *__restrict__ out) {
+    using Gm = V4Geom<LPB, RING>;
+    __shared__ uint32_t lds[kImageBytes / 4];
+    load_image(lds, img);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave);  // group of 64 blocks
+    if (g * 64u >= n_blocks) return;
+#if JL_GV4_WAVETIME
+    const uint64_t wid = g;
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    uint32_t *slot = lds + kV4SlotDword + wave * 64u;
+    const uint64_t dbase = (uint64_t)(uintptr_t)data;
+    const uint32_t do_mask = flags & 1u;
+
+    V4Wave<LPB, NT, RING> W(lds, lane);
+    W.voff = (lane / LPB) * 4096u + (lane % LPB) * 16u;
+    W.lc = 131072u | ((lane & 31u) << 2);
+    W.s_init = (lane % LPB == 0) ? 0xffffffffu : 0u;
+
+    // prefetch cursor: group pg, round pr (first block pg*64 + pr*R)
+    uint64_t pg = g;
+    uint32_t pr = 0;
+    auto rsrc = [&](uint64_t gg, uint32_t rr) -> v4i {
+        const uint64_t b = gg * 64u + (uint64_t)rr * Gm::R;
+        if (b >= n_blocks) return make_rsrc(dbase, 0u);
+        const uint64_t nb = n_blocks - b < (uint64_t)Gm::R ? n_blocks - b : (uint64_t)Gm::R;
+        return make_rsrc(dbase + b * 4096u, (uint32_t)(nb * 4096u));
+    };
+    auto adv = [&](uint64_t &gg, uint32_t &rr) {
+        if (++rr == (uint32_t)LPB || gg * 64u + (uint64_t)rr * Gm::R >= n_blocks) {
+            rr = 0;
+            gg += waves;
+        }
+    };
+    W.cur = rsrc(pg, pr);
+    adv(pg, pr);
+    W.nxt = rsrc(pg, pr);
+    W.prime_all(std::make_integer_sequence<int, Gm::P>());
+
+    uint32_t r = 0;  // round within the group
+    for (;;) {
+        W.round(std::make_integer_sequence<int, Gm::S>());
+        // rotate the prefetch resources: the next round's loads already use nxt
+        W.cur = W.nxt;
+        adv(pg, pr);
+        W.nxt = rsrc(pg, pr);
+        uint32_t crc = W.finish();
+        if (do_mask) crc = mask_crc(crc);
+        if (lane % LPB == 0) slot[r * Gm::R + lane / LPB] = crc;
+        const uint64_t g0 = g * 64u;
+        if (++r == (uint32_t)LPB || g0 + (uint64_t)r * Gm::R >= n_blocks) {
+            const uint32_t res = slot[lane];
+            if (g0 + lane < n_blocks) out[g0 + lane] = res;
+            r = 0;
+            g += waves;
+            if (g * 64u >= n_blocks) break;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (zero-range) loads
+#if JL_GV4_WAVETIME
+    if (lane == 0 && wid < 16384u) {
+        g_fx_wt[2u * wid] = wt0;
+        g_fx_wt[2u * wid + 1u] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+}
+
+#endif
 
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
                              int grid, hipStream_t st) {

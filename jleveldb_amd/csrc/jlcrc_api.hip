@@ -1233,7 +1233,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     const size_t hn = jlk::kLCCounters * ng + 1;
     const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
                  o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
-                 o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_end = o_res + 256;
+                 o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_end = o_dl + al(nb * 4);
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
     // The dense blocks' runs of events (lc_dense): no more runs than events, and
@@ -1269,6 +1269,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.dense_off = (uint64_t *)(ws + o_do);
     A.cap_flag = (uint32_t *)(ws + o_flag);
     A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
+    A.dense_ctr = (uint32_t *)(ws + o_flag + 16);
+    A.dense_list = (uint32_t *)(ws + o_dl);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
     A.stash_pool = pool;
@@ -1280,6 +1282,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
+    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 8, st));  // lc_walk appends to the dense list at once
     JL_HIP(jlk::launch_lc_walk(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});

@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         *A.stash_ctr = 0;
     }
     uint32_t cnt = 0;
+    bool listed = false;  // a dense block: appended to lc_dense's list below
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
         const uint64_t bs = b * 32768u, be = bs + 32768u < A.size ? bs + 32768u : A.size;
@@ -253,8 +254,20 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
             }
             atomicAdd(&h[wv][kLCOver], 1u);
             cnt = kLCDense;
+            listed = true;
         }
         A.count[b] = cnt;
+    }
+    {  // the dense blocks into lc_dense's list: one global atomic per wave that has any
+        const uint64_t dm = __builtin_amdgcn_ballot_w64(listed);
+        if (dm) {
+            const uint32_t lane = threadIdx.x & 63u;
+            uint32_t base = 0;
+            if (lane == (uint32_t)__builtin_ctzll(dm)) base = atomicAdd(&A.dense_ctr[0], (uint32_t)__builtin_popcountll(dm));
+            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)__builtin_ctzll(dm));
+            if (listed)
+                A.dense_list[base + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] = (uint32_t)b;
+        }
     }
     __syncthreads();
     // the LDS slots out, the workgroup's 256 blocks together: consecutive threads
@@ -650,31 +663,44 @@ __device__ __forceinline__ uint32_t ld_zk(const uint32_t *tab, uint32_t x, uint3
 }
 // z(s) through T0 (one zero byte)
 __device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { return (s >> 8) ^ T0[s & 0xffu]; }
-// A workgroup's dense blocks: the candidates blockIdx.x + j * gridDim.x, 64 of
-// them per wave-wide load of count[] (the ballot of the dense ones is kept, so a
-// log of dense blocks costs one load per 64 blocks and a log without any costs
-// n_blocks / (64 grid) loads per workgroup).
+// A workgroup's dense blocks come from lc_walk's list (dense_list[0 .. dense_ctr[0])),
+// kLDChunk entries at a time from the counter dense_ctr[1], so a workgroup that
+// runs faster takes more blocks (r4; r3 dealt the blocks statically,
+// blockIdx.x + j gridDim.x, and the 4 workgroups of a CU do not run at the same
+// rate: on the DBBench set they finished between 0.92 and 1.34 ms,
+// profiles/r4i_ldprof.json).  The next chunk is always taken one chunk ahead and
+// its list entries loaded then, so no wave waits for the counter or the list.
+constexpr uint32_t kLDChunk = 8;
 struct LDSched {
-    uint64_t base, mask;
-    uint32_t step;
-    __device__ __forceinline__ uint64_t scan(const LCArgs &A) const {
-        const uint64_t i = base + (uint64_t)(threadIdx.x & 63u) * step;
-        return __builtin_amdgcn_ballot_w64(i < A.n_blocks && A.count[i] == kLCDense);
+    uint32_t nd;        // dense blocks listed
+    uint32_t cur, nxt;  // list index of the current / next chunk (>= nd: none)
+    uint32_t curb, nxtb;  // lane k < kLDChunk: their k-th block
+    uint32_t idx;       // the current chunk's next entry
+    __device__ __forceinline__ uint32_t load(const LCArgs &A, uint32_t c) const {
+        const uint32_t k = c + (threadIdx.x & 63u);
+        return (threadIdx.x & 63u) < kLDChunk && c < nd && k < nd ? A.dense_list[k] : 0u;
     }
-    __device__ __forceinline__ void init(const LCArgs &A) {
-        step = gridDim.x;
-        base = blockIdx.x;
-        mask = scan(A);
+    __device__ __forceinline__ void init(const LCArgs &A, uint32_t c0, uint32_t c1) {
+        cur = c0;
+        nxt = c1;
+        curb = load(A, cur);
+        nxtb = load(A, nxt);
+        idx = 0;
     }
-    __device__ __forceinline__ uint64_t next(const LCArgs &A) {  // n_blocks when done
-        while (!mask) {
-            base += 64ull * step;
-            if (base >= A.n_blocks) return A.n_blocks;
-            mask = scan(A);
+    // the next block (n_blocks when done); *moved: the current chunk was exhausted and
+    // the next one taken over (the caller then starts the grab of the one after)
+    __device__ __forceinline__ uint64_t next(const LCArgs &A, uint32_t s_new, bool *moved) {
+        *moved = false;
+        if (idx == kLDChunk || cur + idx >= nd) {
+            cur = nxt;
+            curb = nxtb;
+            nxt = s_new;
+            nxtb = load(A, nxt);
+            idx = 0;
+            *moved = true;
         }
-        const uint32_t j = (uint32_t)__builtin_ctzll(mask);
-        mask &= mask - 1u;
-        return base + (uint64_t)j * step;
+        if (cur + idx >= nd) return A.n_blocks;
+        return (uint32_t)__builtin_amdgcn_readlane((int)curb, (int)idx++);
     }
 };
 // a block can be loaded with whole 16-B vector loads (full, 16-B aligned)
@@ -752,7 +778,12 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t s_m[3];          // per trip (mod 3): first failing candidate
     __shared__ uint32_t s_bad;           // header offset of the block's first failing record
     __shared__ unsigned long long s_seg;  // stash offset of the pass's segment (~0: did not fit)
+    __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
+    const uint32_t nd = uni(A.dense_ctr[0]);
+    if (nd == 0) return;  // no dense block in the log
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    if (t == 0)
+        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], kLDChunk);
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
@@ -770,8 +801,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     const uint32_t W0 = A.seed0;
     const uint32_t C1 = ld_zk(N4, W0 << 8), C2 = ld_zk(N4, W0 << 16), C3 = ld_zk(N4, W0 << 24);
     LDSched sch;
-    sch.init(A);
-    uint64_t b = sch.next(A);
+    sch.nd = nd;
+    sch.init(A, s_c[0], s_c[1]);
+    bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
+    uint32_t grabbed = 0;
+    uint64_t b = sch.next(A, s_c[2], &moved);
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
@@ -800,7 +834,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         if (t < 4) dat[8192 + t] = 0;
         if (t == 0) s_bad = kLCNone;
         ld_sync();
-        const uint64_t bn = sch.next(A);  // its bytes load during this block's work
+        const uint64_t bn = sch.next(A, s_c[2], &moved);  // its bytes load during this block's work
+        if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
+            grabbed = atomicAdd(&A.dense_ctr[1], kLDChunk);
+            grab = true;
+        }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
         LD_T(tb);
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
@@ -899,6 +937,10 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             LD_T(td);
             // ---- stash the pass's runs: one segment (+ a link slot when a pass follows)
             if (t == 0) {
+                if (grab) {  // read by the next block's sch.next (after this pass's barriers)
+                    s_c[2] = grabbed;
+                    grab = false;
+                }
                 const uint64_t n = nr + (done ? 0u : 1u);
                 unsigned long long off = ~0ull;
                 if (!fit) {
