@@ -101,7 +101,8 @@ const char *jl_version(void);
  *                            the measured crossover of the per-call latencies
  *                            (one table)
  *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
- *                            default 12 MiB (one WAL)
+ *                            default 8 MiB (the measured crossover; one ~4 MiB
+ *                            WAL stays on the host)
  * Study builds only (make STUDY=1): JL_OPT_GV4_VARIANT (crc_gv4_kernel bound-study variants). */
 #define JL_OPT_GENERAL_PATH 1
 #define JL_OPT_STREAM_DEPTH 2

@@ -209,14 +209,15 @@ int get_ws(Workspace **out) {
 // Host-memory calls touching fewer bytes than these run on the calling thread's
 // SSE4.2 path (host_paths.cpp): below them the device round trip (copies,
 // launches, synchronisation) costs more than the CRC itself.  Measured per-call
-// latencies (bench.py "dispatch", r3b; pageable input, one caller): a table of
-// ~4.2 KB blocks breaks even at 2 MiB (148 vs 145 us) and the device wins from
-// 4 MiB (227 vs 286 us); a WAL of 1 056-B records costs the device more (the
-// walk's ~12 launches): host 259 vs device 361 us at 4 MiB, 510 vs 658 at
-// 8 MiB, device ahead from 16 MiB (638 vs 803).  So the reference's own call
-// sizes — one <= 2 MiB table at open, one <= 4 MiB WAL at recovery — stay on
-// the host, batches of tables and large logs go to the device.
-constexpr int64_t kHostThresholdDefault = 2 << 20, kLogHostThresholdDefault = 12 << 20;
+// latencies (bench.py "dispatch", r4j, pageable input, one caller; r4 staging
+// copies on a persistent thread pool and polled completion): a table of ~4.2 KB
+// blocks costs the device 105 us against the host's 74 at 1 MiB and 128 against
+// 146 at 2 MiB, so jleveldb's tables (>= 2 MiB, Options.java:208) go to the
+// device; a WAL of 1 056-B records costs the device 303 against 259 us at
+// 4 MiB and 469 against 515 at 8 MiB (its ~10 launches and the walk's dependent
+// header loads cost ~130 us at any size), so the reference's ~4 MiB WAL
+// (Options.java:203) stays on the host and logs from 8 MiB go to the device.
+constexpr int64_t kHostThresholdDefault = 2 << 20, kLogHostThresholdDefault = 8 << 20;
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
 // batch takes and its tuning.  Defaults are the measured best; tests force the

@@ -180,16 +180,19 @@ def _wal(oracle, payload, n, seed, n_flips):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["dump", "dump-default"])
-@pytest.mark.parametrize("shape", ["c1_1056", "dbbench_131"])
+@pytest.mark.parametrize("shape", ["c1_1056", "dbbench_131", "wal_4mib"])
 def test_jni_verify_log_vs_oracle(harness, oracle, tmp_path, mode, shape):
-    """Crc32CShims.verifyLog on a C1-shaped WAL (1 056-B records, 40 MiB) and a
+    """Crc32CShims.verifyLog on a C1-shaped WAL (1 056-B records, 40 MiB), a
     DBBench-shaped one (131-B records: every 32 KiB block dense, so lc_dense runs
     under JNI; 16 MiB, which also makes verifyLog's first capacity guess too
-    small and the grow path run), each with byte flips, checksum on and off."""
+    small and the grow path run) and one WAL of the reference's size (~4 MiB
+    write buffer, Options.java:203: the host path at the default threshold),
+    each with byte flips, checksum on and off."""
     from jleveldb_amd import workloads
 
-    payload, n = ((workloads.C1_PAYLOAD, (40 << 20) // 1063) if shape == "c1_1056"
-                  else (workloads.DBBENCH_PAYLOAD, (16 << 20) // 138))
+    payload, n = {"c1_1056": (workloads.C1_PAYLOAD, (40 << 20) // 1063),
+                  "dbbench_131": (workloads.DBBENCH_PAYLOAD, (16 << 20) // 138),
+                  "wal_4mib": (workloads.C1_PAYLOAD, (4 << 20) // 1063)}[shape]
     log = _wal(oracle, payload, n, 21, 9)
     p = tmp_path / "wal.log"
     p.write_bytes(log)
