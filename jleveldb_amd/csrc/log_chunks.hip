@@ -258,18 +258,21 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         }
         A.count[b] = cnt;
     }
-    {  // the dense blocks into lc_dense's list: one global atomic per wave that has any
-        const uint64_t dm = __builtin_amdgcn_ballot_w64(listed);
-        if (dm) {
-            const uint32_t lane = threadIdx.x & 63u;
-            uint32_t base = 0;
-            if (lane == (uint32_t)__builtin_ctzll(dm)) base = atomicAdd(&A.dense_ctr[0], (uint32_t)__builtin_popcountll(dm));
-            base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)__builtin_ctzll(dm));
-            if (listed)
-                A.dense_list[base + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] = (uint32_t)b;
-        }
-    }
+    // the dense blocks into lc_dense's list: the waves' counts summed in LDS, one
+    // global atomic per workgroup that has any (one per wave cost the DBBench set's
+    // walk ~20 us: 2 048 atomics on one address at the same moment)
+    __shared__ uint32_t s_dn, s_db;
+    if (threadIdx.x == 0) s_dn = 0;
     __syncthreads();
+    const uint64_t dm = __builtin_amdgcn_ballot_w64(listed);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t woff = 0;
+    if (dm && lane == 0) woff = atomicAdd(&s_dn, (uint32_t)__builtin_popcountll(dm));
+    woff = (uint32_t)__builtin_amdgcn_readfirstlane((int)woff);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_dn) s_db = atomicAdd(&A.dense_ctr[0], s_dn);
+    __syncthreads();
+    if (listed) A.dense_list[s_db + woff + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] = (uint32_t)b;
     // the LDS slots out, the workgroup's 256 blocks together: consecutive threads
     // store a block's consecutive slots (a run of kLCLdsSlots x 8 B per block; one
     // thread per block writing its own slots touched 64 lines per store, 33 us of
@@ -762,6 +765,11 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 #ifndef JL_LD_PROF
 #define JL_LD_PROF 0
 #endif
+// The walk (and a block's staging) at a higher wave priority than the crc phase:
+// its dependent LDS trips then queue behind fewer of the other workgroups' lookups
+#ifndef JL_LD_PRIO
+#define JL_LD_PRIO 1
+#endif
 #if JL_LD_PROF
 __device__ unsigned long long g_ld_prof[4096 * 8];
 #define LD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
@@ -841,6 +849,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
         LD_T(tb);
+#if JL_LD_PRIO
+        __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
+#endif
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
         uint64_t seg0 = ~0ull;      // thread 0: the block's first segment (stash offset | entries << 48)
         uint64_t link = ~0ull;      // thread 0: the previous segment's link slot
@@ -886,6 +897,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 p += m * (7u + d0.length);
             }
             ld_sync();  // the pass's runs are in LDS
+#if JL_LD_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             LD_T(tc);
             // ---- crc: one thread per OK record (none once the block has a failure:
             // the records after it are dropped whatever their crc)
@@ -974,6 +988,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 A.stash[so + t] = ld_run_entry(run_a[t], run_b[t], next - first);
             }
             total += nev;
+#if JL_LD_PRIO
+            if (!done) __builtin_amdgcn_s_setprio(2);
+#endif
             if (!done) ld_sync();  // the next pass's walk rewrites the runs
 #if JL_LD_PROF
             LD_T(te);
