@@ -765,10 +765,10 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 #ifndef JL_LD_PROF
 #define JL_LD_PROF 0
 #endif
-// The walk (and a block's staging) at a higher wave priority than the crc phase:
+// The walk and a block's staging (2; 1: the walk only) at a higher wave priority than the crc phase:
 // its dependent LDS trips then queue behind fewer of the other workgroups' lookups
 #ifndef JL_LD_PRIO
-#define JL_LD_PRIO 1
+#define JL_LD_PRIO 2
 #endif
 #if JL_LD_PROF
 __device__ unsigned long long g_ld_prof[4096 * 8];
@@ -827,6 +827,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
+#if JL_LD_PRIO >= 2
+        __builtin_amdgcn_s_setprio(2);
+#endif
         ld_sync();  // the previous block's readers of dat / runs / s_* are done
         if (ld_vec(A, b)) {
             pre.store(dat, t);
@@ -915,6 +918,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
                     const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
                     const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
+                    // s below is z^(4 - tl)(state) when the last dword was padded: the
+                    // stored crc's state shifted the same way (ahead of the chains, so its
+                    // dependent lookups overlap theirs)
+                    uint32_t want = ~unmask_crc(lds32u(dat, h));
+                    for (uint32_t z = tl ? 4u - tl : 0u; z; z--) want = ld_z1(t0, want);
                     // the first dword, seeded (C_h folds in the seed dword before it)
                     uint32_t d = dat[a];
                     if (nd == 1u) d &= tmask;
@@ -941,10 +949,6 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                         for (uint32_t c = 0; c < 4; c++) y[c] = ld_zk(N16, y[c], v[c]);
                     }
                     const uint32_t s = ld_zk(N16, y[0]) ^ ld_zk(N12, y[1]) ^ ld_zk(N8, y[2]) ^ ld_zk(N4, y[3]);
-                    // s = z^(4 - tl)(state) when the last dword was padded: compare with
-                    // the stored crc's state shifted the same way
-                    uint32_t want = ~unmask_crc(lds32u(dat, h));
-                    for (uint32_t z = tl ? 4u - tl : 0u; z; z--) want = ld_z1(t0, want);
                     if (s != want) atomicMin(&s_bad, h);
                 }
             }
