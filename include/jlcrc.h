@@ -93,6 +93,10 @@ const char *jl_version(void);
  *                            directly (the default), 0 = copy pageable input
  *                            through pinned staging buffers
  *   JL_OPT_STAGE_THREADS     host threads copying pageable input into staging (8)
+ *   JL_OPT_STAGE_PIECE       staged copies: bytes per piece handed to the copy
+ *                            engine while the host copies the next piece (a
+ *                            chunk of <= 4 pieces' worth goes in 4 MiB pieces;
+ *                            0 = one piece per chunk).  Default 16 MiB
  *   JL_OPT_HOST_THRESHOLD    host-memory entry points jl_crc32c_fixed / _batch and
  *                            jl_table_verify: a call touching fewer bytes than
  *                            this runs on the calling thread's SSE4.2 path
@@ -112,6 +116,7 @@ const char *jl_version(void);
 #define JL_OPT_STAGE_THREADS 6
 #define JL_OPT_HOST_THRESHOLD 7
 #define JL_OPT_LOG_HOST_THRESHOLD 8
+#define JL_OPT_STAGE_PIECE 9
 #define JL_OPT_GV4_VARIANT 101
 #define JL_PATH_AUTO 0
 #define JL_PATH_STREAM 1

@@ -211,6 +211,7 @@ def shutdown() -> None:
 
 OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 3, 4
 OPT_HOST_REGISTER, OPT_STAGE_THREADS, OPT_HOST_THRESHOLD, OPT_LOG_HOST_THRESHOLD = 5, 6, 7, 8
+OPT_STAGE_PIECE = 9
 OPT_GV4_VARIANT = 101  # study builds only
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
 

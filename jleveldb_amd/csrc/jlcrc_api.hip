@@ -229,6 +229,7 @@ struct Options {
     int64_t split_cap = -1;           // JL_OPT_SPLIT_CAP: chunks of split blocks (-1: min(2^20, 2048 n))
     int host_register = 1;            // JL_OPT_HOST_REGISTER: pin pageable inputs >= 64 MiB for the call
     int stage_threads = 8;            // JL_OPT_STAGE_THREADS: host threads copying into pinned staging
+    int64_t stage_piece = 16 << 20;   // JL_OPT_STAGE_PIECE: staged copy pieces of big chunks (0: whole chunk)
     int64_t host_threshold = kHostThresholdDefault;  // JL_OPT_HOST_THRESHOLD: smaller host-memory calls run on the host
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
     int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
@@ -350,8 +351,13 @@ int slot_put_data(Slot &sl, const HostSrc &src, uint64_t off, uint64_t bytes) {
     }
     JL_HIP(hipEventSynchronize(sl.copied));  // the staging buffer's previous copy is done
     JL_HIP(sl.h_data.ensure(bytes));
-    for (uint64_t a = 0; a < bytes; a += kStagePiece) {
-        const uint64_t m = std::min(kStagePiece, bytes - a);
+    // small chunks (one call's latency) in 4 MiB pieces; big ones in stage_piece
+    // pieces: every piece is one job for the copy threads, and 16 jobs per 64 MiB
+    // chunk cost the staged C2 stream ~1/3 of its rate (r4q 20.5 vs r3 ~30 GiB/s)
+    const uint64_t sp = (uint64_t)opt().stage_piece;
+    const uint64_t piece = bytes <= 4 * kStagePiece ? kStagePiece : (sp ? sp : bytes);
+    for (uint64_t a = 0; a < bytes; a += piece) {
+        const uint64_t m = std::min(piece, bytes - a);
         par_memcpy((uint8_t *)sl.h_data.p + a, p + a, m);
         JL_HIP(hipMemcpyAsync((uint8_t *)sl.d_in.p + a, (const uint8_t *)sl.h_data.p + a, m, hipMemcpyHostToDevice, sl.st));
     }
@@ -725,6 +731,10 @@ int jl_set_option(int option, int64_t value) {
         if (value < 0) break;
         o.host_threshold = value;
         return JL_OK;
+    case JL_OPT_STAGE_PIECE:
+        if (value < 0 || (value > 0 && value < (1 << 20))) break;
+        o.stage_piece = value;
+        return JL_OK;
     case JL_OPT_LOG_HOST_THRESHOLD:
         if (value < 0) break;
         o.log_host_threshold = value;
@@ -752,6 +762,7 @@ int64_t jl_get_option(int option) {
     case JL_OPT_STAGE_THREADS: return o.stage_threads;
     case JL_OPT_HOST_THRESHOLD: return o.host_threshold;
     case JL_OPT_LOG_HOST_THRESHOLD: return o.log_host_threshold;
+    case JL_OPT_STAGE_PIECE: return o.stage_piece;
     case JL_OPT_GV4_VARIANT: return o.gv4_variant;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
     }

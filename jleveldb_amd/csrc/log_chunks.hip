@@ -613,8 +613,9 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // default 100-B values make ~237 records of 138 B per 32 KiB block).  Cutting
 // them into 8-chunk rounds would pay a round epilogue per ~2 windows, so a
 // workgroup takes the whole block instead (persistent grid over the blocks
-// lc_walk marked, 3 workgroups of 256 threads per CU; the next dense block's
-// 32 KiB load into registers while the current one is worked on):
+// lc_walk listed, 4 workgroups of 256 threads per CU, blocks taken in chunks of
+// kLDChunk from a global counter; the next dense block's 32 KiB load into
+// registers while the current one is worked on):
 //   stage  the block into LDS
 //   walk   RUNS of records: the header at p is read by every thread, thread t
 //          checks the candidate header at p + (t + 1) L (L = 7 + its length) —
@@ -622,11 +623,10 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 //          candidate (ballot, LDS min) ends the run: a run of equal records
 //          (DBBench's) is walked 257 headers per trip, one barrier each
 //          (J/db/LogReader.java:297-383, the reference's decisions in its order)
-//   crc    one thread per OK record, table lookups that never conflict: the
-//          state advances a dword at a time through 8 nibble tables
-//          N_i[v] = z^4(v << 4i), 32 copies interleaved so lane l reads bank
-//          l mod 32 (r3's byte tables, one copy beside the staged block, spent
-//          58 % of the LDS cycles in bank conflicts, profiles/r3n_pmc_lc_dense.json);
+//   crc    one thread per OK record, table lookups that never conflict (ld_zk:
+//          nibble tables, one copy each): the record's dwords end-aligned in
+//          groups of 4, four chains (position c of every group) stepping z^16,
+//          folded at the end with z^16 / z^12 / z^8 / z^4;
 //          the record's first bytes are seeded with W0 (the 4 bytes before it
 //          that take state 0 to value()'s 0xffffffff, so the first dword needs
 //          no byte tables), its last dword is zero-padded and the stored crc

@@ -149,3 +149,28 @@ def test_log_layout_matches_logwriter(jl, oracle, dest_length):
         img[h:h + 7] = ref[h:h + 7]  # CRC bytes are the device's job; framing is checked here
         img[h + 7:h + 7 + n] = src[so:so + n]
     assert bytes(img) == ref  # everything outside the fragments is zero trailer
+
+
+def test_options_round_trip_and_ranges(jl):
+    """jl_set_option / jl_get_option: every option keeps a valid value and refuses
+    out-of-range ones (JL_ERR_INVALID, the previous value kept); no device needed."""
+    cases = [  # option, valid values, invalid values
+        (jl.OPT_HOST_REGISTER, [0, 1], [2, -1]),
+        (jl.OPT_STAGE_THREADS, [1, 8, 64], [0, 65]),
+        (jl.OPT_HOST_THRESHOLD, [0, 2 << 20], [-1]),
+        (jl.OPT_LOG_HOST_THRESHOLD, [0, 8 << 20], [-1]),
+        (jl.OPT_STAGE_PIECE, [0, 1 << 20, 16 << 20], [-1, 4096]),
+    ]
+    for opt, good, bad in cases:
+        prev = jl.get_option(opt)
+        try:
+            for v in good:
+                jl.set_option(opt, v)
+                assert jl.get_option(opt) == v
+            for v in bad:
+                with pytest.raises(Exception):
+                    jl.set_option(opt, v)
+                assert jl.get_option(opt) == good[-1]
+        finally:
+            jl.set_option(opt, prev)
+    assert jl.get_option(jl.OPT_STAGE_PIECE) == 16 << 20
