@@ -306,6 +306,38 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 // entries behind, reads the same sequence back.  The counter and queues sit in
 // dwords [kGvDynDword, +257) of the LDS image, unused by both gv4 images (zero
 // when the image is loaded).
+// With a device counter (GV4Args::deal, zeroed before the kernel: by gv4_scan,
+// or the log path's memset) only the heaviest 1/kGvStaticDiv of the rounds go by
+// the stride; past them the workgroup's counter indexes BATCHES of kGvDealBatch
+// consecutive rounds that the workgroups take from the device counter as they go
+// (r4): the static stride balanced the waves of a CU but not the XCDs — on C3 the workgroups of four XCDs finished ~100 us after
+// the other four's (XCD means 1 797-1 945 us, sigma ~14 us within an XCD; on the
+// C5 mixed set the other four XCDs were the late ones; wave ends of r4l,
+// tools/gv4_wavetime.py), and the kernel lasts until its slowest XCD.  The wave
+// that opens batch b takes batch b + 1 from the device counter (the first one
+// takes batches 0 and 1), so a batch's base is normally known before its first
+// round is asked for; a wave that finds it missing waits on its tag in LDS.  The
+// atomic's return makes the compiler wait vmcnt(0) (it cannot count the ring's
+// asm loads), once per batch.  One device atomic per ROUND instead (batches of
+// 2-8 rounds per wave) serialised on the counter's address: C5 1 056-B 0.97 ->
+// 1.2-3.3 ms; batches from the first round on put C3's heaviest rounds on a few
+// workgroups (64 per batch: 2.0 -> 2.43 ms), hence the static head.  Without a
+// counter (implicit rounds), the stride above.
+#ifndef JL_GV4_DEAL
+#define JL_GV4_DEAL 1
+#endif
+#ifndef JL_GV4_DEAL_BATCH
+#define JL_GV4_DEAL_BATCH 32
+#endif
+// batch size min(kGvDealBatch, R / (64 G)): every workgroup still takes >= ~48
+// batches (the tail's granularity), and a call of fewer than 64 G rounds keeps
+// the stride (its batches would leave most CUs idle)
+constexpr uint32_t kGvDealBatch = JL_GV4_DEAL_BATCH;
+#ifndef JL_GV4_STATIC_DIV
+#define JL_GV4_STATIC_DIV 4
+#endif
+constexpr uint32_t kGvStaticDiv = JL_GV4_STATIC_DIV;
+constexpr uint32_t kGvBatchDword = 7900;  // 16 slots {base, tag = batch + 1}: free in both gv4 images (zero)
 constexpr uint32_t kGvNoRound = 0xffffffffu;  // >= any round count (< 2^31)
 constexpr uint32_t kGvDynDword = 7935;       // [0] the workgroup's counter, then 16 queues of 16 rounds
 
@@ -319,6 +351,9 @@ struct GPF {
     uint32_t i;            // r = seq(i)
     uint32_t made;         // rounds taken into the queue so far (seq(i) for i < made is known)
     uint32_t *ctr, *Q;     // LDS: the workgroup's counter, this wave's queue
+    uint32_t *deal;        // the device counter (null: the workgroup's)
+    uint32_t J0;           // with deal: counter values below J0 take the stride, j G + bx
+    uint32_t DB;           // with deal: rounds per batch
     uint32_t e, E, K;
     uint32_t k;      // sequence number of the current round (descriptor set k & 1)
     bool vec_next;   // the next round's descriptor was issued into set (k+1) & 1
@@ -331,9 +366,36 @@ struct GPF {
     // is asked for (i == made), read back from the queue after that
     __device__ __forceinline__ uint32_t seq(uint32_t i_) {
         if (i_ < made) return uni(Q[i_ & 15u]);
+        const bool lane0 = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u;
         uint32_t j = 0;
-        if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0u) j = atomicAdd(ctr, 1u);
+        if (lane0) j = atomicAdd(ctr, 1u);
         j = uni(j);
+        if (JL_GV4_DEAL && deal && j >= J0) {  // batches of rounds from the device counter
+            const uint32_t k = j - J0, X0 = J0 * G;
+            const uint32_t b = k / DB, o = k - b * DB;
+            volatile uint32_t *slot = ctr + (kGvBatchDword - kGvDynDword);
+            if (o == 0u) {  // opens batch b: take batch b + 1 (b = 0: batches 0 and 1)
+                const uint32_t n = b == 0u ? 2u * DB : DB;
+                uint32_t g = 0;
+                if (lane0) g = atomicAdd(deal, n);
+                g = uni(g);
+                if (lane0) {
+                    if (b == 0u) {
+                        slot[0] = g;
+                        slot[1] = 1u;
+                        g += DB;
+                    }
+                    slot[2u * ((b + 1u) & 15u)] = g;  // base before tag: LDS writes of a wave land in order
+                    slot[2u * ((b + 1u) & 15u) + 1u] = b + 2u;
+                }
+            }
+            while (uni(slot[2u * (b & 15u) + 1u]) != b + 1u) __builtin_amdgcn_s_sleep(1);
+            const uint64_t x = (uint64_t)X0 + uni(slot[2u * (b & 15u)]) + o;
+            const uint32_t rr = x < R ? R - 1u - (uint32_t)x : kGvNoRound;
+            Q[made & 15u] = rr;
+            made++;
+            return rr;
+        }
         const uint64_t x = (uint64_t)j * G + bx;
         const uint32_t rr = x < R ? R - 1u - (uint32_t)x : kGvNoRound;  // heaviest first
         Q[made & 15u] = rr;  // every lane writes the same value
@@ -395,6 +457,9 @@ struct GPF {
                                          uint32_t lane, uint64_t dmy) {
         ctr = lds + kGvDynDword;
         Q = lds + kGvDynDword + 1u + 16u * (threadIdx.x >> 6);
+        DB = nr / (64u * g) < kGvDealBatch ? nr / (64u * g) : kGvDealBatch;
+        deal = DB ? A.deal : nullptr;
+        J0 = nr / (kGvStaticDiv * g);
         made = 0;
         G = g;
         bx = b;
@@ -1078,7 +1143,8 @@ __global__ __launch_bounds__(1024) void gv4_scan_kernel(const uint32_t *hist, ui
     }
     if (t == 0) {  // solo blocks (>= kGSoloKey steps, any K): one round each, after all others
         rstart[kGSoloKey] = carry;
-        *n_rounds = carry + hist[kGSoloKey];
+        n_rounds[0] = carry + hist[kGSoloKey];
+        n_rounds[1] = 0;  // crc_gv4_kernel's round counter (GV4Args::deal)
     }
     for (uint32_t j = t; j < hist[kGSoloKey]; j += 1024u) gv4_null_groups(desc, (uint64_t)carry + j, 1u);
 }

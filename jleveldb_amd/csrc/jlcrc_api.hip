@@ -654,6 +654,7 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     A.parts = parts;
     A.desc = desc;
     A.n_rounds = n_rounds;
+    A.deal = n_rounds + 1;  // zeroed by gv4_scan_kernel
     if (e == hipSuccess) e = gv4_launch(A, st);
     if (e == hipSuccess && SP.part_cap) e = jlk::launch_gv4_combine(P, SP, parts, st);
     (void)hipFreeAsync(buf, st);
@@ -1294,7 +1295,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
-    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 8, st));  // lc_walk appends to the dense list at once
+    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));  // lc_walk appends to the dense list at once; gv4 round counter
     JL_HIP(jlk::launch_lc_walk(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
@@ -1326,6 +1327,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         G.P.out32 = A.first_bad;
         G.desc = A.desc;
         G.n_rounds = A.rstart + jlk::kLCBins;
+        G.deal = A.dense_ctr + 2;  // zeroed with dense_ctr before lc_walk
         G.seed0 = jlmath::slice4_inv(0xffffffffu);
         G.parts = A.parts;
         G.study = (uint32_t)opt().gv4_variant;  // 0 unless a study build set JL_OPT_GV4_VARIANT

@@ -77,6 +77,7 @@ struct GV4Args {
     uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
     uint32_t study;             // study build only: crc_gv4_kernel variant (0 = the product kernel)
     uint32_t *parts;            // split blocks: raw chunk states (group idx = kGPart | part index)
+    uint32_t *deal;             // rounds counter, zero at launch (null: each workgroup deals its own)
 };
 // A block above kGSplitMin (MODE_CRC) is cut into m <= 2048 chunks of S bytes
 // (S a multiple of 128, >= 64 KiB; the last chunk shorter) computed as blocks of
