@@ -664,6 +664,26 @@ __device__ __forceinline__ uint32_t ld_zk(const uint32_t *tab, uint32_t x, uint3
     }
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], w));
 }
+// JL_LD_T5: the same maps from 5-bit tables, z^(4k)(x) = XOR_i F_k,i[(x >> 5i) & 31]
+// (i = 0..6, the last field 2 bits).  A 32-entry table fills the 32 banks a
+// ds_read_b32 lane group sees, so these never conflict either, and a dword costs
+// 7 lookups instead of 8 (2 VALU each for the address instead of 1 v_perm).
+#ifndef JL_LD_T5
+#define JL_LD_T5 1
+#endif
+constexpr uint32_t kLDTabDwords = JL_LD_T5 ? 7u * 32u : 128u;  // one map's tables
+__device__ __forceinline__ uint32_t ld_zk5(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
+    uint32_t r[7];
+    r[0] = *(const uint32_t *)((const char *)tab + ((x << 2) & 0x7cu));
+#pragma unroll
+    for (uint32_t i = 1; i < 7; i++)
+        r[i] = *(const uint32_t *)((const char *)tab + 128u * i + ((x >> (5u * i - 2u)) & 0x7cu));
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ w);
+}
+__device__ __forceinline__ uint32_t ld_map(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
+    if (JL_LD_T5) return ld_zk5(tab, x, w);
+    return ld_zk(tab, x, w);
+}
 // z(s) through T0 (one zero byte)
 __device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { return (s >> 8) ^ T0[s & 0xffu]; }
 // A workgroup's dense blocks come from lc_walk's list (dense_list[0 .. dense_ctr[0])),
@@ -779,7 +799,7 @@ __device__ unsigned long long g_ld_prof[4096 * 8];
 
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t nt[4 * 128];      // nibble tables of z^4, z^8, z^12, z^16 (ld_zk)
+    __shared__ uint32_t nt[4 * kLDTabDwords];  // tables of z^4, z^8, z^12, z^16 (ld_map)
     __shared__ uint32_t t0[256];
     __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
     __shared__ uint32_t run_b[kLDRuns];  // first event (of the pass) | type << 16 | kind << 24
@@ -795,19 +815,22 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
-    for (uint32_t w = t; w < 4u * 128u; w += kLDThreads) {  // N_k,i[v] = z^(4k)(v << 4i) at 128 (k-1) + 16 i + v
-        const uint32_t k = (w >> 7) + 1u, i = (w >> 4) & 7u, v = w & 15u;
-        uint32_t s = v << (4u * i);
+    for (uint32_t w = t; w < 4u * kLDTabDwords; w += kLDThreads) {
+        // nibbles: N_k,i[v] = z^(4k)(v << 4i) at 128 (k-1) + 16 i + v; 5 bits: F_k,i[v] =
+        // z^(4k)(v << 5i) at 224 (k-1) + 32 i + v (i = 6: v < 4, the rest unused)
+        const uint32_t k = w / kLDTabDwords + 1u, e = w % kLDTabDwords;
+        const uint32_t i = JL_LD_T5 ? e >> 5 : e >> 4, v = JL_LD_T5 ? e & 31u : e & 15u;
+        uint32_t s = JL_LD_T5 ? (i * 5u < 32u ? v << (5u * i) : 0u) : v << (4u * i);
         for (uint32_t z = 0; z < 4u * k; z++) s = ld_z1(t0, s);
         nt[w] = s;
     }
     ld_sync();
-    const uint32_t *N4 = nt, *N8 = nt + 128, *N12 = nt + 256, *N16 = nt + 384;
+    const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords, *N12 = nt + 2 * kLDTabDwords, *N16 = nt + 3 * kLDTabDwords;
     // the first dword of a record whose crc range starts q & 3 = h bytes into a
     // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
     // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
     const uint32_t W0 = A.seed0;
-    const uint32_t C1 = ld_zk(N4, W0 << 8), C2 = ld_zk(N4, W0 << 16), C3 = ld_zk(N4, W0 << 24);
+    const uint32_t C1 = ld_map(N4, W0 << 8), C2 = ld_map(N4, W0 << 16), C3 = ld_map(N4, W0 << 24);
     LDSched sch;
     sch.nd = nd;
     sch.init(A, s_c[0], s_c[1]);
@@ -946,9 +969,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                         for (uint32_t c = 0; c < 4; c++) v[c] = D[4u * g + c];
                         if (g + 1u == G) v[3] &= tmask;
 #pragma unroll
-                        for (uint32_t c = 0; c < 4; c++) y[c] = ld_zk(N16, y[c], v[c]);
+                        for (uint32_t c = 0; c < 4; c++) y[c] = ld_map(N16, y[c], v[c]);
                     }
-                    const uint32_t s = ld_zk(N16, y[0]) ^ ld_zk(N12, y[1]) ^ ld_zk(N8, y[2]) ^ ld_zk(N4, y[3]);
+                    const uint32_t s = ld_map(N16, y[0]) ^ ld_map(N12, y[1]) ^ ld_map(N8, y[2]) ^ ld_map(N4, y[3]);
                     if (s != want) atomicMin(&s_bad, h);
                 }
             }
@@ -1034,7 +1057,7 @@ extern "C" int jl_study_ld_prof(unsigned long long *out) {
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * 128 * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
