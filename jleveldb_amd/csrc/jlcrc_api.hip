@@ -1245,7 +1245,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t hn = jlk::kLCCounters * ng + 1;
     const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
-                 o_rs = o_hscan + al(hn * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
+                 o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
+                 o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_end = o_dl + al(nb * 4);
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
@@ -1277,6 +1278,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.start = (uint64_t *)(ws + o_start);
     A.hist = (uint32_t *)(ws + o_hist);
     A.hscan = (uint32_t *)(ws + o_hscan);
+    A.rowtot = (uint32_t *)(ws + o_rt);
+    A.tstat = (uint64_t *)(ws + o_ts);
     A.rstart = (uint32_t *)(ws + o_rs);
     A.first_bad = (uint32_t *)(ws + o_fb);
     A.dense_off = (uint64_t *)(ws + o_do);
@@ -1298,13 +1301,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));  // lc_walk appends to the dense list at once; gv4 round counter
     JL_HIP(jlk::launch_lc_walk(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
-    hipcub::TransformInputIterator<uint64_t, U32ToU64, const uint32_t *> it(A.count, U32ToU64{});
-    size_t t1 = 0, t2 = 0;
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, it, A.start, (int)(nb + 1), st));
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, A.hist, A.hscan, (int)hn, st));
-    JL_HIP(c.ws_tmp.ensure(std::max(t1, t2)));
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t1, it, A.start, (int)(nb + 1), st));
-    JL_HIP(hipcub::DeviceScan::ExclusiveSum(c.ws_tmp.p, t2, A.hist, A.hscan, (int)hn, st));
+    JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:
     // <= kLCSlots records in a block that is not dense, and a block's bytes bound its extra chunks
     A.round_cap = nb * (jlk::kLCSlots + 10) / 8 + jlk::kLCBins + 1;

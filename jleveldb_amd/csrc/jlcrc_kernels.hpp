@@ -157,8 +157,10 @@ struct LCArgs {
     uint64_t stash_pool;
     unsigned long long *stash_ctr;  // zeroed by lc_walk
     uint64_t *start;       // n_blocks + 1: exclusive scan of count
-    uint32_t *hist;        // kLCCounters * n_grp + 1, counter-major (hist[c * n_grp + group])
-    uint32_t *hscan;       // its exclusive scan
+    uint32_t *hist;        // kLCCounters * n_grp, counter-major (hist[c * n_grp + group])
+    uint32_t *hscan;       // per counter (row): exclusive scan over the groups (lc_scan)
+    uint32_t *rowtot;      // kLCCounters: the rows' totals
+    uint64_t *tstat;       // lc_scan's tile look-back statuses (zeroed by lc_walk)
     uint32_t *rstart;      // kLCBins + 1: first round of every bin; [kLCBins] = rounds
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
     uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range
@@ -177,6 +179,7 @@ struct LCArgs {
     const uint32_t *aux;
 };
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st);
+hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
@@ -186,6 +189,9 @@ uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
+constexpr uint32_t kLSTile = 4096;  // lc_scan: values per workgroup and step
+// decoupled look-back statuses (lc_scan): 0 = not yet, else a flag | value
+constexpr uint64_t kLDAgg = 1ull << 62, kLDInc = 1ull << 63, kLDVal = kLDAgg - 1;
 
 // block i of an offset/length batch lies (with its stored crc in MODE_TABLE_VERIFY)
 // inside the caller's base_bytes

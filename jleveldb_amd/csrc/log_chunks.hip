@@ -171,6 +171,21 @@ __device__ __forceinline__ uint64_t lc_hop(const uint8_t *p, uint64_t rem) {
     return lc_header(p, rem);
 }
 
+// Exclusive prefix sum over the wave's 64 lanes with DPP only (no LDS
+// crossbar round trips): Hillis-Steele inside each row of 16 (row_shr 1/2/4/8),
+// then the row totals through row_bcast:15 (rows 1, 3) and row_bcast:31 (rows
+// 2, 3).  Lanes without a source add the `old` operand, 0.  All lanes active.
+__device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
+    uint32_t x = v;
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x - v;
+}
+
 // Adds one (s = 1) or removes one (s = ~0u) record of geometry g to the chunk
 // histogram of its walk group: its chunks by bin, plus one multi-chunk record
 // and its J parts when J > 1.
@@ -204,12 +219,12 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
     if (b == 0) {
         A.count[A.n_blocks] = 0;
-        A.hist[(uint64_t)kLCCounters * A.n_grp] = 0;
         *A.cap_flag = 0;
         *A.stash_ctr = 0;
     }
     uint32_t cnt = 0;
     bool listed = false;  // a dense block: appended to lc_dense's list below
+    if (b < (A.n_blocks + kLSTile) / kLSTile) A.tstat[b] = 0;  // lc_scan's look-back statuses
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
         const uint64_t bs = b * 32768u, be = bs + 32768u < A.size ? bs + 32768u : A.size;
@@ -289,6 +304,106 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     }
 }
 
+// The two scans of a verification in one launch (r4; before, two rocprim scans,
+// ~24 us on every C5 set):
+//   * workgroups [0, tiles): start = exclusive scan of count[0 .. n_blocks] (u32 ->
+//     u64), tiles of kLSTile with a decoupled look-back (tstat, zeroed by lc_walk);
+//   * the next kLCCounters: counter c's row of hist (its per-group counts) scanned
+//     on its own, hscan[c n_grp + g] = the groups before g, rowtot[c] = the row's
+//     total — all that lc_setup / lc_build / lc_combine / lc_finish use (a scan
+//     across the rows gave the same numbers as differences).
+// Tile / row chunks pass through LDS (coalesced loads and stores); every thread
+// scans 16 consecutive values, the 256 thread totals by wave DPP sums.
+__device__ __forceinline__ uint32_t ls_block_excl(uint32_t v, uint32_t *wsum, uint32_t *total) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    const uint32_t ex = lc_wave_excl_sum(v);
+    if (lane == 63u) wsum[wv] = ex + v;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (uint32_t w = 0; w < 4u; w++) {
+        before += w < wv ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    *total = tot;
+    __syncthreads();  // wsum reused by the next call
+    return before + ex;
+}
+__global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
+    __shared__ uint32_t buf[kLSTile];
+    __shared__ uint32_t wsum[4];
+    __shared__ unsigned long long s_pre;
+    const uint32_t t = threadIdx.x;
+    const uint32_t tiles = (A.n_blocks + kLSTile) / kLSTile;  // n_blocks + 1 values
+    if (blockIdx.x < tiles) {
+        const uint64_t k = blockIdx.x, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
+        for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
+        __syncthreads();
+        uint32_t v[16], s = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {
+            v[j] = buf[16u * t + j];
+            s += v[j];
+        }
+        uint32_t agg;
+        const uint32_t ex = ls_block_excl(s, wsum, &agg);
+        if (t == 0) {
+            uint64_t P = 0;
+            if (k == 0) {
+                __hip_atomic_store(&A.tstat[0], kLDInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(&A.tstat[k], kLDAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int64_t q = (int64_t)k - 1; q >= 0; q--) {
+                    uint64_t w;
+                    while ((w = __hip_atomic_load(&A.tstat[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+                        __builtin_amdgcn_s_sleep(1);
+                    P += w & kLDVal;
+                    if (w & kLDInc) break;
+                }
+                __hip_atomic_store(&A.tstat[k], kLDInc | (P + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_pre = P;
+        }
+        __syncthreads();
+        const uint64_t pre = s_pre;
+        uint32_t run = ex;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {  // exclusive values back into LDS, in place
+            buf[16u * t + j] = run;
+            run += v[j];
+        }
+        __syncthreads();
+        for (uint32_t j = t; j < kLSTile; j += 256u)
+            if (base + j < n) A.start[base + j] = pre + buf[j];
+        return;
+    }
+    const uint32_t c = blockIdx.x - tiles;  // a hist row
+    const uint64_t nw = A.n_grp, row = (uint64_t)c * nw;
+    uint32_t carry = 0;
+    for (uint64_t g0 = 0; g0 < nw; g0 += kLSTile) {
+        for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = g0 + j < nw ? A.hist[row + g0 + j] : 0u;
+        __syncthreads();
+        uint32_t v[16], s = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {
+            v[j] = buf[16u * t + j];
+            s += v[j];
+        }
+        uint32_t tot;
+        uint32_t run = carry + ls_block_excl(s, wsum, &tot);
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) {
+            buf[16u * t + j] = run;
+            run += v[j];
+        }
+        __syncthreads();
+        for (uint32_t j = t; j < kLSTile; j += 256u)
+            if (g0 + j < nw) A.hscan[row + g0 + j] = buf[j];
+        carry += tot;
+        __syncthreads();  // buf reused
+    }
+    if (t == 0) A.rowtot[c] = carry;
+}
+
 // rstart[k] = rounds of the bins before k (ceil(count/8) rounds each; bin k =
 // chunks of K = k/16 + 1 windows with tail pads d = k mod 16 (mod 16)),
 // rstart[kLCBins] = all rounds (clamped to the descriptor capacity, cap_flag set
@@ -296,8 +411,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
 __global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
     __shared__ uint32_t wsum[kLCBins / 64];
     const uint32_t k = threadIdx.x, lane = k & 63u, wv = k >> 6;
-    const uint64_t nw = A.n_grp;
-    const uint32_t cnt = A.hscan[(k + 1) * nw] - A.hscan[k * nw];
+    const uint32_t cnt = A.rowtot[k];
     const uint32_t rounds = (cnt + 7u) / 8u;
     uint32_t incl = rounds;  // inclusive scan: waves, then across the 8 wave sums
     for (uint32_t o = 1; o < 64u; o <<= 1) {
@@ -428,20 +542,6 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
 // 8 blocks per wave, all their loads issued first (r2: 8 waves x 8 blocks ran
 // lc_build 77 -> 63 us against 4 x 16, C5 ~3 % faster; 16 x 4 about the same)
 constexpr uint32_t kLCBuildWaves = JL_LC_BUILD_WAVES;
-// Exclusive prefix sum over the wave's 64 lanes with DPP only (no LDS
-// crossbar round trips): Hillis-Steele inside each row of 16 (row_shr 1/2/4/8),
-// then the row totals through row_bcast:15 (rows 1, 3) and row_bcast:31 (rows
-// 2, 3).  Lanes without a source add the `old` operand, 0.  All lanes active.
-__device__ __forceinline__ uint32_t lc_wave_excl_sum(uint32_t v) {
-    uint32_t x = v;
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return x - v;
-}
 
 // A dense block's events from its runs (lc_dense's stash segments): a wave takes
 // 64 runs at a time (lane = run: its count, exclusive prefix over the lanes),
@@ -499,7 +599,7 @@ __device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint
 __device__ __forceinline__ void lc_finish(const LCArgs &A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.result[0] = A.start[A.n_blocks];
-        A.result[1] = A.hscan[(uint64_t)kLCCounters * A.n_grp] - A.hscan[(uint64_t)kLCOver * A.n_grp];
+        A.result[1] = A.rowtot[kLCOver];
         A.result[2] = *A.cap_flag;
     }
 }
@@ -508,7 +608,7 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
     __shared__ uint32_t ctr[kLCCounters], rs[kLCBins + 1];
     const uint64_t nw = A.n_grp;
     for (uint32_t i = threadIdx.x; i < kLCCounters; i += blockDim.x)
-        ctr[i] = A.checksum ? A.hscan[i * nw + blockIdx.x] - A.hscan[i * nw] : 0u;
+        ctr[i] = A.checksum ? A.hscan[i * nw + blockIdx.x] : 0u;
     for (uint32_t i = threadIdx.x; i <= kLCBins && A.checksum; i += blockDim.x) rs[i] = A.rstart[i];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -567,8 +667,7 @@ __device__ __forceinline__ uint32_t lc_zshift(const uint32_t *aux, uint32_t v, u
 }
 
 __global__ __launch_bounds__(256) void lc_combine_kernel(LCArgs A, uint32_t n_big_max) {
-    const uint64_t nw = A.n_grp;
-    const uint32_t nbig = A.hscan[(kLCBig + 1u) * nw] - A.hscan[kLCBig * nw];
+    const uint32_t nbig = A.rowtot[kLCBig];
     const uint32_t lim = nbig < n_big_max ? nbig : n_big_max;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
         const LCBig g = A.big[i];
@@ -1067,6 +1166,11 @@ hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
 
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
     hipLaunchKernelGGL(lc_walk_kernel, dim3((A.n_grp + 3) / 4), dim3(256), 0, st, A);
+    return hipGetLastError();
+}
+hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st) {
+    const uint32_t tiles = (A.n_blocks + kLSTile) / kLSTile;
+    hipLaunchKernelGGL(lc_scan_kernel, dim3(tiles + kLCCounters), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st) {

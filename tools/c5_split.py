@@ -16,8 +16,8 @@ import sys
 
 
 def short(name):
-    if "rocprim" in name:
-        return "scans (rocprim)"
+    if "rocprim" in name or "lc_scan_kernel" in name:
+        return "scans"
     if "crc_gv4_kernel<5" in name:
         return "crc_gv4_kernel<LOG_CHUNK>"
     for k in ("lc_walk", "lc_dense", "lc_build", "lc_setup", "lc_combine", "lc_apply"):
