@@ -210,13 +210,14 @@ __device__ __forceinline__ void lc_hist(uint32_t *h, const LCGeom &g, uint32_t s
 // makes every hop also wait for the store's acknowledgement (gfx9 counts stores
 // in vmcnt, and the compiler waits vmcnt(0) with a store outstanding).
 constexpr uint32_t kLCLdsSlots = 34;
-__global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
+__global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A, uint32_t wg0) {
     __shared__ uint32_t h[4][kLCCounters];
     __shared__ uint64_t ls[256][kLCLdsSlots + 1];  // [thread][slot], padded: the write-back reads it in order
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t b = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint32_t wg = wg0 + blockIdx.x;  // this launch's first workgroup (JL_LC_WALK_SPLIT)
+    const uint64_t b = (uint64_t)wg * 256u + threadIdx.x;
     if (b == 0) {
         A.count[A.n_blocks] = 0;
         *A.cap_flag = 0;
@@ -292,12 +293,12 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     // store a block's consecutive slots (a run of kLCLdsSlots x 8 B per block; one
     // thread per block writing its own slots touched 64 lines per store, 33 us of
     // the C5 walk).  Slots past a block's count are never read.
-    const uint64_t b0 = (uint64_t)blockIdx.x * 256u;
+    const uint64_t b0 = (uint64_t)wg * 256u;
     for (uint32_t e = threadIdx.x; e < 256u * kLCLdsSlots; e += 256u) {
         const uint32_t t = e / kLCLdsSlots, j = e - t * kLCLdsSlots;
         if (b0 + t < A.n_blocks) A.slots[(b0 + t) * kLCSlots + j] = ls[t][j];
     }
-    const uint64_t g0 = (uint64_t)blockIdx.x * 4u;
+    const uint64_t g0 = (uint64_t)wg * 4u;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) {
         const uint32_t g = i % 4u, c = i / 4u;  // 4 consecutive groups of one counter: one 16-B run
         if (g0 + g < A.n_grp) A.hist[(uint64_t)c * A.n_grp + g0 + g] = h[g][c];
@@ -1164,8 +1165,20 @@ hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Study (JL_LC_WALK_SPLIT = S > 1): the walk as S launches over consecutive block
+// ranges, fewer hop chains in flight over a smaller part of the log at a time
+#ifndef JL_LC_WALK_SPLIT
+#define JL_LC_WALK_SPLIT 1
+#endif
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
-    hipLaunchKernelGGL(lc_walk_kernel, dim3((A.n_grp + 3) / 4), dim3(256), 0, st, A);
+    const uint32_t W = (A.n_grp + 3) / 4, S = JL_LC_WALK_SPLIT;
+    if (S > 1 && W >= 64u * S) {
+        const uint32_t per = (W + S - 1) / S;
+        for (uint32_t w0 = 0; w0 < W; w0 += per)
+            hipLaunchKernelGGL(lc_walk_kernel, dim3(W - w0 < per ? W - w0 : per), dim3(256), 0, st, A, w0);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(lc_walk_kernel, dim3(W), dim3(256), 0, st, A, 0u);
     return hipGetLastError();
 }
 hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st) {
