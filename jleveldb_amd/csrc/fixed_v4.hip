@@ -178,10 +178,17 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
     const uint64_t rounds = (n_blocks + Gm::R - 1) / Gm::R;
     uint32_t *ctr = lds + kFxDynDword;
     // the workgroup's next round (kFxNone past its last), taken from the counter
+    // JL_FX_DYN 2: the workgroup owns a contiguous range of rounds instead (its
+    // waves stream one region, as the static groups do)
+    const uint64_t per = (rounds + gridDim.x - 1) / gridDim.x;
     auto take = [&]() -> uint32_t {
         uint32_t j = 0;
         if (lane == 0) j = atomicAdd(ctr, 1u);
         j = uni(j);
+        if (JL_FX_DYN == 2) {
+            const uint64_t rr = (uint64_t)blockIdx.x * per + j;
+            return j < per && rr < rounds ? (uint32_t)rr : kFxNone;
+        }
         const uint64_t rr = (uint64_t)j * gridDim.x + blockIdx.x;
         return rr < rounds ? (uint32_t)rr : kFxNone;
     };
