@@ -189,7 +189,10 @@ uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
-constexpr uint32_t kLSTile = 4096;  // lc_scan: values per workgroup and step
+#ifndef JL_LS_TILE
+#define JL_LS_TILE 4096  // study builds: 256 runs the multi-tile / multi-step paths on small logs
+#endif
+constexpr uint32_t kLSTile = JL_LS_TILE;  // lc_scan: values per workgroup and step (256 threads x kLSTile / 256)
 // decoupled look-back statuses (lc_scan): 0 = not yet, else a flag | value
 constexpr uint64_t kLDAgg = 1ull << 62, kLDInc = 1ull << 63, kLDVal = kLDAgg - 1;
 

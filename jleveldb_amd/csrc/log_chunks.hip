@@ -329,6 +329,8 @@ __device__ __forceinline__ uint32_t ls_block_excl(uint32_t v, uint32_t *wsum, ui
     __syncthreads();  // wsum reused by the next call
     return before + ex;
 }
+constexpr uint32_t kLSPer = kLSTile / 256u;  // values per thread
+static_assert(kLSTile % 256u == 0u, "kLSTile: a multiple of the workgroup");
 __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
     __shared__ uint32_t buf[kLSTile];
     __shared__ uint32_t wsum[4];
@@ -339,10 +341,10 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
         const uint64_t k = blockIdx.x, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
         for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
         __syncthreads();
-        uint32_t v[16], s = 0;
+        uint32_t v[kLSPer], s = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {
-            v[j] = buf[16u * t + j];
+        for (uint32_t j = 0; j < kLSPer; j++) {
+            v[j] = buf[kLSPer * t + j];
             s += v[j];
         }
         uint32_t agg;
@@ -368,8 +370,8 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
         const uint64_t pre = s_pre;
         uint32_t run = ex;
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {  // exclusive values back into LDS, in place
-            buf[16u * t + j] = run;
+        for (uint32_t j = 0; j < kLSPer; j++) {  // exclusive values back into LDS, in place
+            buf[kLSPer * t + j] = run;
             run += v[j];
         }
         __syncthreads();
@@ -383,17 +385,17 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
     for (uint64_t g0 = 0; g0 < nw; g0 += kLSTile) {
         for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = g0 + j < nw ? A.hist[row + g0 + j] : 0u;
         __syncthreads();
-        uint32_t v[16], s = 0;
+        uint32_t v[kLSPer], s = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {
-            v[j] = buf[16u * t + j];
+        for (uint32_t j = 0; j < kLSPer; j++) {
+            v[j] = buf[kLSPer * t + j];
             s += v[j];
         }
         uint32_t tot;
         uint32_t run = carry + ls_block_excl(s, wsum, &tot);
 #pragma unroll
-        for (uint32_t j = 0; j < 16u; j++) {
-            buf[16u * t + j] = run;
+        for (uint32_t j = 0; j < kLSPer; j++) {
+            buf[kLSPer * t + j] = run;
             run += v[j];
         }
         __syncthreads();
