@@ -179,15 +179,27 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
     uint32_t *ctr = lds + kFxDynDword;
     // the workgroup's next round (kFxNone past its last), taken from the counter
     // JL_FX_DYN 2: the workgroup owns a contiguous range of rounds instead (its
-    // waves stream one region, as the static groups do)
+    // waves stream one region, as the static groups do); 3: the same, each wave
+    // taking kFxSpan consecutive rounds at a time (a contiguous stretch per wave)
+    constexpr uint32_t kFxSpan = JL_FX_DYN == 3 ? 4u : 1u;
     const uint64_t per = (rounds + gridDim.x - 1) / gridDim.x;
+    uint32_t span_next = 0, span_left = 0;  // uniform: the wave's next round of its stretch
     auto take = [&]() -> uint32_t {
+        if (JL_FX_DYN == 3 && span_left) {
+            span_left--;
+            return span_next++;
+        }
         uint32_t j = 0;
         if (lane == 0) j = atomicAdd(ctr, 1u);
         j = uni(j);
-        if (JL_FX_DYN == 2) {
-            const uint64_t rr = (uint64_t)blockIdx.x * per + j;
-            return j < per && rr < rounds ? (uint32_t)rr : kFxNone;
+        if (JL_FX_DYN >= 2) {
+            const uint64_t j0 = (uint64_t)j * kFxSpan, rr = (uint64_t)blockIdx.x * per + j0;
+            if (j0 >= per || rr >= rounds) return kFxNone;
+            const uint64_t lim = (per - j0 < kFxSpan ? per - j0 : kFxSpan);
+            const uint64_t n = rounds - rr < lim ? rounds - rr : lim;
+            span_next = (uint32_t)rr + 1u;
+            span_left = (uint32_t)n - 1u;
+            return (uint32_t)rr;
         }
         const uint64_t rr = (uint64_t)j * gridDim.x + blockIdx.x;
         return rr < rounds ? (uint32_t)rr : kFxNone;
