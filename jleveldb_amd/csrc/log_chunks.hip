@@ -788,6 +788,9 @@ __device__ __forceinline__ uint32_t ld_map(const uint32_t *tab, uint32_t x, uint
 }
 // z(s) through T0 (one zero byte)
 __device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { return (s >> 8) ^ T0[s & 0xffu]; }
+// z^-1(s) through Ti[b] = (T0[i] << 8) | i, i the byte whose T0 entry has top byte b
+// (z(r) = (r >> 8) ^ T0[r & 0xff] keeps T0's top byte, a permutation of i)
+__device__ __forceinline__ uint32_t ld_zi1(const uint32_t *Ti, uint32_t s) { return (s << 8) ^ Ti[s >> 24]; }
 // A workgroup's dense blocks come from lc_walk's list (dense_list[0 .. dense_ctr[0])),
 // kLDChunk entries at a time from the counter dense_ctr[1], so a workgroup that
 // runs faster takes more blocks (r4; r3 dealt the blocks statically,
@@ -927,6 +930,12 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         nt[w] = s;
     }
     ld_sync();
+    {  // t0 becomes the inverse table (ld_zi1): the stored crc is shifted back instead
+        const uint32_t e = t0[t];
+        ld_sync();
+        t0[e >> 24] = (e << 8) | t;
+    }
+    ld_sync();
     const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords, *N12 = nt + 2 * kLDTabDwords, *N16 = nt + 3 * kLDTabDwords;
     // the first dword of a record whose crc range starts q & 3 = h bytes into a
     // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
@@ -1043,11 +1052,13 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
                     const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
                     const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
-                    // s below is z^(4 - tl)(state) when the last dword was padded: the
-                    // stored crc's state shifted the same way (ahead of the chains, so its
-                    // dependent lookups overlap theirs)
+                    // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last
+                    // dword was padded with 4 - tl zeros (tl = 0: the state): so u =
+                    // z^-tl(stored state), tl = 0: z^-4 (inverse byte steps, ahead of the
+                    // chains, so their dependent lookups overlap the chains'; one z^4 fold
+                    // of 7 lookups less per record)
                     uint32_t want = ~unmask_crc(lds32u(dat, h));
-                    for (uint32_t z = tl ? 4u - tl : 0u; z; z--) want = ld_z1(t0, want);
+                    for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(t0, want);
                     // the first dword, seeded (C_h folds in the seed dword before it)
                     uint32_t d = dat[a];
                     if (nd == 1u) d &= tmask;
@@ -1073,7 +1084,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
 #pragma unroll
                         for (uint32_t c = 0; c < 4; c++) y[c] = ld_map(N16, y[c], v[c]);
                     }
-                    const uint32_t s = ld_map(N16, y[0]) ^ ld_map(N12, y[1]) ^ ld_map(N8, y[2]) ^ ld_map(N4, y[3]);
+                    const uint32_t s = ld_map(N12, y[0]) ^ ld_map(N8, y[1]) ^ ld_map(N4, y[2]) ^ y[3];
                     if (s != want) atomicMin(&s_bad, h);
                 }
             }
