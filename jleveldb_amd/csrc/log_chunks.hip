@@ -1005,7 +1005,18 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     break;
                 }
                 uint32_t m = 1;
+                bool run = false;  // uniform: the record after p repeats it (a run to measure)
                 if (!d0.stop) {
+                    const uint32_t c1 = p + 7u + d0.length;
+                    if (c1 < blen && blen - c1 >= 7u) {
+                        const LCDecision d1 = lc_decide(blen - c1, eof, lds32u(dat, c1 + 3u));
+                        run = d1.kind == 1u && d1.length == d0.length && d1.type == d0.type;
+                    }
+                }
+                // a record the next one does not repeat (a block's leading fragment,
+                // a length change) is a run of 1 with no trip (r4: DBBench blocks then
+                // take one barrier trip instead of two or three)
+                if (run) {
                     const uint32_t L = 7u + d0.length, c = p + (t + 1u) * L;
                     bool ok = false;
                     if (c < blen && blen - c >= 7u) {
