@@ -950,7 +950,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     uint64_t b = sch.next(A, s_c[2], &moved);
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
-    unsigned long long pool_lo = 0, pool_hi = 0;  // thread 0: this workgroup's unused stash entries
+    unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
     uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
 #if JL_LD_PROF
     uint64_t acc[5] = {0, 0, 0, 0, 0};
@@ -990,8 +990,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
 #endif
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
-        uint64_t seg0 = ~0ull;      // thread 0: the block's first segment (stash offset | entries << 48)
-        uint64_t link = ~0ull;      // thread 0: the previous segment's link slot
+        uint64_t seg0 = ~0ull;      // uniform: the block's first segment (stash offset | entries << 48)
+        uint64_t link = ~0ull;      // uniform: the previous segment's link slot
         bool fit = true, done = false;
         while (!done) {
             // the block's failure so far: read before this pass's crc atomics can change it
@@ -1100,39 +1100,42 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 }
             }
             LD_T(td);
-            // ---- stash the pass's runs: one segment (+ a link slot when a pass follows)
-            if (t == 0) {
-                if (grab) {  // read by the next block's sch.next (after this pass's barriers)
-                    s_c[2] = grabbed;
-                    grab = false;
-                }
-                const uint64_t n = nr + (done ? 0u : 1u);
-                unsigned long long off = ~0ull;
-                if (!fit) {
-                } else if (!A.stash_pool) {
-                    off = atomicAdd(A.stash_ctr, (unsigned long long)n);
+            // ---- stash the pass's runs: one segment (+ a link slot when a pass follows).
+            // The stash state is uniform (every thread tracks it); thread 0's atomic
+            // reaches the others through LDS only when a pool is refilled (every ~69
+            // DBBench blocks) or, without pools (small logs), for every pass: no
+            // barrier in this phase otherwise (r4)
+            if (t == 0 && grab) {  // read by the next block's sch.next (after its barriers)
+                s_c[2] = grabbed;
+                grab = false;
+            }
+            const uint64_t n = nr + (done ? 0u : 1u);
+            unsigned long long so = ~0ull;
+            if (fit) {
+                if (!A.stash_pool) {
+                    if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)n);
+                    ld_sync();
+                    so = s_seg;
                 } else {  // a pass needs at most kLDRuns + 1 <= kLDPool entries
                     if (pool_hi - pool_lo < n) {
-                        pool_lo = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
+                        if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
+                        ld_sync();
+                        pool_lo = s_seg;
                         pool_hi = pool_lo + A.stash_pool;
                     }
-                    off = pool_lo;
+                    so = pool_lo;
                     pool_lo += n;
                 }
-                if (fit && off + n > A.stash_cap) {  // past the stash: the caller's event array is too small
+                if (so + n > A.stash_cap) {  // past the stash: the caller's event array is too small
                     fit = false;
-                    off = ~0ull;
-                } else if (!fit) {
+                    so = ~0ull;
                 } else if (link != ~0ull) {
-                    A.stash[link] = (kLDLink << 56) | (n << 40) | off;
+                    if (t == 0) A.stash[link] = (kLDLink << 56) | (n << 40) | so;
                 } else {
-                    seg0 = off | (n << 48);
+                    seg0 = so | (n << 48);
                 }
-                link = done || !fit ? ~0ull : off + nr;
-                s_seg = off;
             }
-            ld_sync();
-            const unsigned long long so = s_seg;
+            link = done || !fit ? ~0ull : so + nr;
             if (t < nr && so != ~0ull) {
                 const uint32_t first = run_b[t] & 0xffffu;
                 const uint32_t next = t + 1u < nr ? run_b[t + 1u] & 0xffffu : nev;
