@@ -217,3 +217,37 @@ def test_gv4_concurrent_streams(gpu, jl, oracle):
         want = oracle.batch(*batches[s], threads=THREADS)
         for o in outs[s]:
             assert np.array_equal(u32(o), want)
+
+
+def test_gv4_table_verify_batched_rounds(gpu, jl, oracle):
+    """A table of 400 000 blocks (~50 000 rounds: past 64 x the grid, so the
+    rounds after the heaviest quarter are dealt in batches from the device
+    counter, general_v4.hip GPF::seq) through MODE_TABLE_VERIFY: trailers written
+    by jl_table_trailers_dev (a sample pinned to the oracle's TableBuilder
+    trailer), every block verifies; bytes flipped in 64 blocks (data or trailer)
+    fail exactly those."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    n = 400_000
+    sizes = rng.integers(0, 3000, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(sizes.astype(np.uint64) + 5)[:-1]
+    total = int(off[-1]) + int(sizes[-1]) + 5
+    d_f = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu)
+    d_off, d_size = to_dev(off.view(np.int64), gpu), to_dev(sizes.view(np.int32), gpu)
+    types = rng.integers(0, 2, n, dtype=np.uint8)
+    tr = jl.table_trailers_dev(d_f, d_off, d_size, types=to_dev(types, gpu)).reshape(-1, 5)
+    idx = (d_off + d_size.to(torch.int64)).unsqueeze(1) + torch.arange(5, device=gpu).unsqueeze(0)
+    d_f[idx.reshape(-1)] = tr.reshape(-1)  # the file now holds each block's trailer
+    host = d_f.cpu().numpy()
+    for i in rng.integers(0, n, 200):
+        o, s = int(off[i]), int(sizes[i])
+        assert host[o + s:o + s + 5].tobytes() == oracle.table_trailer(host[o:o + s].tobytes(), int(types[i])), i
+    assert jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy().all()
+    bad = np.unique(rng.integers(0, n, 64))
+    for i in bad:
+        o, s = int(off[i]), int(sizes[i])
+        d_f[o + int(rng.integers(0, s + 5))] ^= 1 << int(rng.integers(0, 8))
+    st = jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy()
+    assert set(np.nonzero(st == 0)[0].tolist()) == set(bad.tolist())
