@@ -1247,7 +1247,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
                  o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
-                 o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_end = o_dl + al(nb * 4);
+                 o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
+                 o_end = o_nl + al(nb * 4);
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
     // The dense blocks' runs of events (lc_dense): no more runs than events, and
@@ -1287,6 +1288,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
     A.dense_ctr = (uint32_t *)(ws + o_flag + 16);
     A.dense_list = (uint32_t *)(ws + o_dl);
+    A.nlong = (uint32_t *)(ws + o_nl);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
     A.stash_pool = pool;

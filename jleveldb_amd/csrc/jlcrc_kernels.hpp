@@ -161,6 +161,7 @@ struct LCArgs {
     uint32_t *hscan;       // per counter (row): exclusive scan over the groups (lc_scan)
     uint32_t *rowtot;      // kLCCounters: the rows' totals
     uint64_t *tstat;       // lc_scan's tile look-back statuses (zeroed by lc_walk)
+    uint32_t *nlong;       // n_blocks: a dense block's long records left to the rounds (zeroed by lc_walk)
     uint32_t *rstart;      // kLCBins + 1: first round of every bin; [kLCBins] = rounds
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
     uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range

@@ -200,6 +200,21 @@ __device__ __forceinline__ void lc_hist(uint32_t *h, const LCGeom &g, uint32_t s
     }
 }
 
+// lc_hist into the global histogram of group grp (lc_dense: a dense block's long
+// records, after lc_walk wrote the groups' counts and before lc_scan reads them)
+__device__ __forceinline__ void lc_hist_global(const LCArgs &A, uint64_t grp, const LCGeom &g) {
+    uint32_t *h = A.hist + grp;
+    const uint64_t nw = A.n_grp;
+    if (g.J == 1u) {
+        atomicAdd(&h[lc_bin(g.K, g.r) * nw], 1u);
+    } else {
+        atomicAdd(&h[lc_bin(kLCWin, 0u) * nw], g.J - 1u);
+        atomicAdd(&h[lc_bin(g.K - kLCWin * (g.J - 1u), g.r) * nw], 1u);
+        atomicAdd(&h[kLCBig * nw], 1u);
+        atomicAdd(&h[kLCPart * nw], g.J);
+    }
+}
+
 // Walk groups of kLCGroup consecutive blocks, one per wave (4 per workgroup).
 // The walk also initialises what later kernels accumulate into (first_bad,
 // count[n_blocks], the scan's zero tail, cap_flag, the stash counter): no memsets.
@@ -228,6 +243,7 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A, uint32_t wg0) {
     if (b < (A.n_blocks + kLSTile) / kLSTile) A.tstat[b] = 0;  // lc_scan's look-back statuses
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
+        A.nlong[b] = 0;  // lc_dense's deferred long records
         const uint64_t bs = b * 32768u, be = bs + 32768u < A.size ? bs + 32768u : A.size;
         const bool eof = be - bs < 32768u;
         const uint64_t base = (uint64_t)(uintptr_t)A.log;
@@ -617,12 +633,13 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     // the wave's blocks wv, wv + 16, ... of the group: all their loads first
     constexpr uint32_t kPer = kLCGroup / kLCBuildWaves;
-    uint32_t cnt[kPer];
+    uint32_t cnt[kPer], nl[kPer];
     uint64_t st[kPer], sl[kPer], doff[kPer];
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         cnt[i] = b < A.n_blocks ? A.count[b] : 0u;  // dense blocks: counted by lc_dense
+        nl[i] = b < A.n_blocks ? A.nlong[b] : 0u;   // dense blocks: long records left to the rounds
         st[i] = b < A.n_blocks ? A.start[b] : 0u;
         doff[i] = b < A.n_blocks ? A.dense_off[b] : kLCNotDense;
     }
@@ -642,8 +659,13 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
         if (b >= A.n_blocks) break;
         if (doff[i] != kLCNotDense) {  // dense block: its events expanded from lc_dense's runs
-            if (doff[i] == ~0ull) continue;  // did not fit: the event array is too small anyway
-            lc_expand_runs(A, b, st[i], doff[i], sl[i]);
+            // (~0: they did not fit, the event array is too small anyway)
+            if (doff[i] != ~0ull) lc_expand_runs(A, b, st[i], doff[i], sl[i]);
+            if (A.checksum && nl[i]) {  // its long records' chunks (lc_dense counted them)
+                const uint64_t s = lane < nl[i] ? A.slots[b * kLCSlots + lane] : 0ull;
+                lc_place_wave(A, ctr, rs, lane < nl[i], b * 32768u + ((uint32_t)s & 0xffffu) + 6u,
+                              1u + (((uint32_t)s >> 16) & 0xffffu), (uint32_t)(s >> 32));
+            }
             continue;
         }
         const uint64_t bs = b * 32768u, s = sl[i];
@@ -902,6 +924,16 @@ __device__ unsigned long long g_ld_prof[4096 * 8];
 #define LD_T(v)
 #endif
 
+// A record of more than kLDLongDw dwords in a dense block is not checked by one
+// thread here: a 31 KiB record after a few short ones held its workgroup ~170 us
+// (a 1 GiB log of such blocks took 40 ms against 0.33 for one record per block,
+// tools/cliff_probe.py).  Its chunks join the rounds instead: counted into its
+// group's histogram (lc_hist_global), its header offset, length and stored crc
+// left in the block's walk slots (nlong[b] of them) for lc_build to place, the
+// crc checked by crc_gv4_kernel<MODE_LOG_CHUNK> / lc_combine, a failure
+// atomicMin'ed into first_bad[b] like the block's own.
+constexpr uint32_t kLDLongDw = 128;
+static_assert(kLDLongDw * 4u * kLCSlots >= 32768u, "a block holds fewer long records than slots");
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
     __shared__ uint32_t nt[4 * kLDTabDwords];  // tables of z^4, z^8, z^12, z^16 (ld_map)
@@ -1062,6 +1094,13 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     const uint32_t h = (ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len);
                     const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
                     const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+                    if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
+                        const uint32_t k = atomicAdd(&A.nlong[b], 1u);  // < kLCSlots: >= 513 B each
+                        A.slots[b * kLCSlots + k] = (uint64_t)h | ((uint64_t)len << 16) |
+                                                    ((uint64_t)lds32u(dat, h) << 32);
+                        lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
+                        continue;
+                    }
                     const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
                     // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last
                     // dword was padded with 4 - tl zeros (tl = 0: the state): so u =

@@ -178,6 +178,26 @@ def test_dense_blocks(gpu, jl, oracle, case):
     assert len(want) > 65
 
 
+@pytest.mark.parametrize("big", [520, 600, 4200, 9000, 31691, 40000])
+def test_dense_blocks_with_long_records(gpu, jl, oracle, big):
+    """Dense blocks (8 short records in their first 4 KiB) that also hold a long
+    record: lc_dense leaves records above kLDLongDw dwords to the rounds (their
+    chunks counted into the group's histogram, placed by lc_build, checked by
+    crc_gv4 / lc_combine); 31 691 B fills a block after ten 100-B records, 40 000
+    fragments across blocks.  Flips in long and short records, clean blocks
+    between, events and read records against the oracle."""
+    rng = np.random.default_rng(big)
+    sizes = ([100] * 10 + [big]) * (6 * 32768 // (10 * 107 + big + 7) + 3) + [100] * 40
+    log = bytearray(oracle.log_write(_payloads(rng, sizes)))
+    per = 10 * 107 + big + 7
+    for k in (1, 4):  # inside a long record, then inside a short one further on
+        log[k * per + 10 * 107 + 7 + int(rng.integers(0, big))] ^= 0x10
+        log[(k + 1) * per + 3 * 107 + 20] ^= 0x01
+    log = bytes(log)
+    want = _check(jl, oracle, log, read_records=True)
+    assert any(e[3] == 2 for e in want)  # a BAD_CRC seen
+
+
 @pytest.mark.parametrize("shift", [1, 3, 8, 15])
 def test_dense_blocks_unaligned_log(gpu, jl, oracle, shift):
     """lc_dense's byte-staging path: a log that does not start on 16 bytes (a
