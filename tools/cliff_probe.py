@@ -45,5 +45,13 @@ def run(lens, reps=10):
 
 ms_m, n_m, b_m = run(mixed)
 ms_s, n_s, b_s = run(single)
+# short records of random lengths (a WAL of variable small values): every block
+# dense, its runs one record long, so lc_dense walks it one header at a time
+rnd = np.random.default_rng(5).integers(0, 201, int(gib * (1 << 30)) // 107).astype(np.uint32)
+ms_r, n_r, b_r = run(rnd)
+dbb = np.full(int(gib * (1 << 30)) // 138, 131, np.uint32)
+ms_d, n_d, b_d = run(dbb)
 print(json.dumps({"blocks": nblk, "short_then_long": {"ms": round(ms_m, 3), "events": n_m, "bytes": b_m},
-                  "one_record_per_block": {"ms": round(ms_s, 3), "events": n_s, "bytes": b_s}}))
+                  "one_record_per_block": {"ms": round(ms_s, 3), "events": n_s, "bytes": b_s},
+                  "random_0_200": {"ms": round(ms_r, 3), "events": n_r, "bytes": b_r},
+                  "dbbench_131": {"ms": round(ms_d, 3), "events": n_d, "bytes": b_d}}))

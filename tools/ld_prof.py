@@ -28,7 +28,9 @@ prof = jl.lib().jl_study_ld_prof
 prof.argtypes = [ctypes.c_void_p]
 buf = np.zeros(4096 * 8, np.uint64)
 dev = torch.device("cuda:0")
-lens = wl.c5_lengths(which)
+# random_0_200: a WAL of variable small values (tools/cliff_probe.py), ~1 GiB
+lens = (np.random.default_rng(5).integers(0, 201, (1 << 30) // 107).astype(np.uint32) if which == "random_0_200"
+        else wl.c5_lengths(which))
 plan = jl.log_layout(wl.packed_offsets(lens), lens)
 src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=dev)
 jl.fill_random_dev(src, wl.SEED + 3)
