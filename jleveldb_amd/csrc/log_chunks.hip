@@ -741,11 +741,12 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // kLDChunk from a global counter; the next dense block's 32 KiB load into
 // registers while the current one is worked on):
 //   stage  the block into LDS
-//   walk   RUNS of records: the header at p is read by every thread, thread t
-//          checks the candidate header at p + (t + 1) L (L = 7 + its length) —
-//          an OK record of the same length and type — and the first failing
-//          candidate (ballot, LDS min) ends the run: a run of equal records
-//          (DBBench's) is walked 257 headers per trip, one barrier each
+//   walk   RUNS of records: the header at p is read by every thread (a scalar
+//          chain); when it repeats the record before it (length and type),
+//          thread t checks the candidate header at p + (t + 1) L (L = 7 + its
+//          length) — an OK record of the same length and type — and the first
+//          failing candidate (ballot, LDS min) ends the run: a run of equal
+//          records (DBBench's) is walked 257 headers per trip, one barrier each
 //          (J/db/LogReader.java:297-383, the reference's decisions in its order)
 //   crc    one thread per OK record, table lookups that never conflict (ld_zk:
 //          nibble tables, one copy each): the record's dwords end-aligned in
@@ -1030,51 +1031,52 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             const bool crc = A.checksum && s_bad == kLCNone;
             // ---- walk: up to kLDRuns runs from p
             uint32_t nr = 0, nev = 0;
+            uint32_t pk = ~0u;  // uniform: the last run's key (below) when its records are OK
             while (nr < kLDRuns) {
-                const LCDecision d0 = lc_decide(blen - p, eof, ld_hdr(dat, blen, p));
-                if (d0.kind == 0) {  // the block's trailer: no event
-                    done = true;
-                    break;
-                }
-                uint32_t m = 1;
-                bool run = false;  // uniform: the record after p repeats it (a run to measure)
-                if (!d0.stop) {
-                    const uint32_t c1 = p + 7u + d0.length;
-                    if (c1 < blen && blen - c1 >= 7u) {
-                        const LCDecision d1 = lc_decide(blen - c1, eof, lds32u(dat, c1 + 3u));
-                        run = d1.kind == 1u && d1.length == d0.length && d1.type == d0.type;
+                // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
+                // end); key = w >> 8 = length | type << 16
+                const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
+                if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
+                    uint32_t m = 1;
+                    if (key == pk) {
+                        // it repeats the record before it: the run is measured from here
+                        // (thread t: the candidate p + (t + 1) L) and joins that record's;
+                        // one header read per record, no peek at the next (r4: records of
+                        // random lengths 6.9 -> 5.3 ms per GiB, tools/cliff_probe.py)
+                        const uint32_t L = 7u + len, c = p + (t + 1u) * L;
+                        const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
+                        const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
+                        const uint32_t slot = trip % 3u;
+                        if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
+                        if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
+                        ld_sync();
+                        const uint32_t f = uni(s_m[slot]);
+                        m = 1u + (f < kLDThreads ? f : kLDThreads);
+                        trip++;
+                    } else {  // a new run (a block's leading fragment, a length change)
+                        if (t == 0) {
+                            run_a[nr] = p | (len << 16);
+                            run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
+                        }
+                        nr++;
                     }
+                    pk = key;
+                    nev += m;
+                    p += m * (7u + len);
+                    continue;
                 }
-                // a record the next one does not repeat (a block's leading fragment,
-                // a length change) is a run of 1 with no trip (r4: DBBench blocks then
-                // take one barrier trip instead of two or three)
-                if (run) {
-                    const uint32_t L = 7u + d0.length, c = p + (t + 1u) * L;
-                    bool ok = false;
-                    if (c < blen && blen - c >= 7u) {
-                        const LCDecision dk = lc_decide(blen - c, eof, lds32u(dat, c + 3u));
-                        ok = dk.kind == 1u && dk.length == d0.length && dk.type == d0.type;
+                // the block's end: the trailer (no event) or a record that stops the walk
+                const LCDecision d0 = lc_decide(rem, eof, rem >= 7u ? w : 0u);
+                if (d0.kind != 0u) {
+                    if (t == 0) {
+                        run_a[nr] = p | (d0.length << 16);
+                        run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
                     }
-                    const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
-                    const uint32_t slot = trip % 3u;
-                    if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
-                    if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
-                    ld_sync();
-                    const uint32_t f = s_m[slot];
-                    m = 1u + (f < kLDThreads ? f : kLDThreads);
-                    trip++;
+                    nr++;
+                    nev++;
                 }
-                if (t == 0) {
-                    run_a[nr] = p | (d0.length << 16);
-                    run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
-                }
-                nr++;
-                nev += m;
-                if (d0.stop) {
-                    done = true;
-                    break;
-                }
-                p += m * (7u + d0.length);
+                done = true;
+                break;
             }
             ld_sync();  // the pass's runs are in LDS
 #if JL_LD_PRIO
