@@ -821,15 +821,27 @@ __device__ __forceinline__ uint32_t ld_zi1(const uint32_t *Ti, uint32_t s) { ret
 // rate: on the DBBench set they finished between 0.92 and 1.34 ms,
 // profiles/r4i_ldprof.json).  The next chunk is always taken one chunk ahead and
 // its list entries loaded then, so no wave waits for the counter or the list.
+// Chunks of kLDChunk blocks, fewer when the list gives a workgroup fewer than 16
+// chunks (ld_chunk): a log of blocks of short records of random lengths (~100 us
+// of walk each) dealt 8 at a time left its workgroups ending 2.26 .. 3.24 ms
+// (profiles/r4bc_walk_variants_ldprof.json)
 constexpr uint32_t kLDChunk = 8;
+#ifndef JL_LD_CHUNK_ADAPT
+#define JL_LD_CHUNK_ADAPT 1
+#endif
+__device__ __forceinline__ uint32_t ld_chunk(uint32_t nd) {
+    const uint32_t c = nd / (16u * gridDim.x);
+    return c < 1u ? 1u : (c > kLDChunk ? kLDChunk : c);
+}
 struct LDSched {
     uint32_t nd;        // dense blocks listed
+    uint32_t ch;        // blocks per chunk (ld_chunk)
     uint32_t cur, nxt;  // list index of the current / next chunk (>= nd: none)
     uint32_t curb, nxtb;  // lane k < kLDChunk: their k-th block
     uint32_t idx;       // the current chunk's next entry
     __device__ __forceinline__ uint32_t load(const LCArgs &A, uint32_t c) const {
         const uint32_t k = c + (threadIdx.x & 63u);
-        return (threadIdx.x & 63u) < kLDChunk && c < nd && k < nd ? A.dense_list[k] : 0u;
+        return (threadIdx.x & 63u) < ch && c < nd && k < nd ? A.dense_list[k] : 0u;
     }
     __device__ __forceinline__ void init(const LCArgs &A, uint32_t c0, uint32_t c1) {
         cur = c0;
@@ -842,7 +854,7 @@ struct LDSched {
     // the next one taken over (the caller then starts the grab of the one after)
     __device__ __forceinline__ uint64_t next(const LCArgs &A, uint32_t s_new, bool *moved) {
         *moved = false;
-        if (idx == kLDChunk || cur + idx >= nd) {
+        if (idx == ch || cur + idx >= nd) {
             cur = nxt;
             curb = nxtb;
             nxt = s_new;
@@ -949,7 +961,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     if (nd == 0) return;  // no dense block in the log
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0)
-        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], kLDChunk);
+        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], JL_LD_CHUNK_ADAPT ? ld_chunk(nd) : kLDChunk);
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
@@ -977,6 +989,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     const uint32_t C1 = ld_map(N4, W0 << 8), C2 = ld_map(N4, W0 << 16), C3 = ld_map(N4, W0 << 24);
     LDSched sch;
     sch.nd = nd;
+    sch.ch = JL_LD_CHUNK_ADAPT ? ld_chunk(nd) : kLDChunk;
     sch.init(A, s_c[0], s_c[1]);
     bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
     uint32_t grabbed = 0;
@@ -1014,7 +1027,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         ld_sync();
         const uint64_t bn = sch.next(A, s_c[2], &moved);  // its bytes load during this block's work
         if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
-            grabbed = atomicAdd(&A.dense_ctr[1], kLDChunk);
+            grabbed = atomicAdd(&A.dense_ctr[1], sch.ch);
             grab = true;
         }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
