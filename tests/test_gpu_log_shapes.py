@@ -104,3 +104,22 @@ def test_block_flips(gpu, jl, oracle, rec):
         log[blk * 32768 + off] ^= 0x01
     w = _check(jl, oracle, log)
     assert int(((w["kind"] != 0) & (w["kind"] != jl.LOG_OK)).sum()) >= 3
+
+
+def test_dense_list_in_chunks_random_lengths(gpu, jl, oracle):
+    """~1.1 GiB of short records of random lengths (0-200 B) with runs of equal
+    ones (mostly 1-3 long, some of 200-600): more than 32 768 dense blocks, so
+    lc_dense takes its list in chunks of 2 (ld_chunk sizes them by the list), and
+    every block walks 300+ runs in passes of 256 with runs that join the record
+    before them (the look-back walk), trips past 257 records included.  Flips in
+    payloads and in a header; every event against the oracle."""
+    rng = np.random.default_rng(SEED + 7)
+    m = (int(1.1 * (1 << 30)) // 107) // 3
+    runs = np.where(rng.random(m) < 0.01, rng.integers(200, 600, m), rng.integers(1, 4, m))
+    lens = np.repeat(rng.integers(0, 201, m), runs).astype(np.uint32)
+    log = _log(jl, gpu, lens)
+    assert log.numel() // 32768 > 32768
+    for at in rng.integers(0, log.numel(), 6):
+        log[int(at)] ^= 0x10
+    w = _check(jl, oracle, log)
+    assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= 1
