@@ -994,6 +994,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
     uint32_t grabbed = 0;
     uint64_t b = sch.next(A, s_c[2], &moved);
+    uint64_t bp = ~0ull;  // the previous block (its first_bad is written once its crc phase is done)
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
@@ -1023,7 +1024,16 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
         }
         if (t < 4) dat[8192 + t] = 0;
-        if (t == 0) s_bad = kLCNone;
+        if (t == 0) {
+            // the previous block's failure, read after the barrier above: its crc
+            // phase ends with no barrier when it was the block's last pass, so a
+            // wave still checking records could atomicMin s_bad after thread 0
+            // had read it at that block's end (r4: a flip in the 178th record of
+            // a 194-record run went unreported, test_dense_list_in_chunks_random_lengths)
+            if (bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
+            s_bad = kLCNone;
+        }
+        bp = b;
         ld_sync();
         const uint64_t bn = sch.next(A, s_c[2], &moved);  // its bytes load during this block's work
         if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
@@ -1214,10 +1224,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         if (t == 0) {
             A.count[b] = total;
             A.dense_off[b] = fit ? seg0 : ~0ull;
-            if (s_bad != kLCNone) A.first_bad[b] = s_bad;
         }
         b = bn;
     }
+    ld_sync();  // the last block's crc phase is done
+    if (t == 0 && bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
 #if JL_LD_PROF
     if (t == 0 && blockIdx.x < 4096u) {
         for (int i = 0; i < 5; i++) g_ld_prof[8u * blockIdx.x + i] = acc[i];
