@@ -251,3 +251,33 @@ def test_gv4_table_verify_batched_rounds(gpu, jl, oracle):
         d_f[o + int(rng.integers(0, s + 5))] ^= 1 << int(rng.integers(0, 8))
     st = jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy()
     assert set(np.nonzero(st == 0)[0].tolist()) == set(bad.tolist())
+
+
+def test_gv4_table_verify_zipf_many_flips(gpu, jl):
+    """2 000 000 blocks of Zipf(1.3) sizes up to 64 KiB (~5.7 GB: C3's size
+    mix), trailers from jl_table_trailers_dev, bits flipped in ~2 000 blocks:
+    the failing set is exactly the flipped blocks, three calls in a row (the
+    round dealing's batches past the heaviest quarter, at C3's scale)."""
+    import torch
+
+    rng = np.random.default_rng(7)
+    n = 2_000_000
+    sizes = np.minimum(rng.zipf(1.3, n), 65536).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(sizes.astype(np.uint64) + 5)[:-1]
+    total = int(off[-1]) + int(sizes[-1]) + 5
+    d_f = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu)
+    d_off, d_size = to_dev(off.view(np.int64), gpu), to_dev(sizes.view(np.int32), gpu)
+    types = rng.integers(0, 2, n, dtype=np.uint8)
+    tr = jl.table_trailers_dev(d_f, d_off, d_size, types=to_dev(types, gpu)).reshape(-1, 5)
+    idx = (d_off + d_size.to(torch.int64)).unsqueeze(1) + torch.arange(5, device=gpu).unsqueeze(0)
+    d_f[idx.reshape(-1)] = tr.reshape(-1)
+    del tr, idx
+    assert jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy().all()
+    bad = np.unique(rng.integers(0, n, 2000))
+    for i in bad:
+        o, s = int(off[i]), int(sizes[i])
+        d_f[o + int(rng.integers(0, s + 5))] ^= 1 << int(rng.integers(0, 8))
+    for _ in range(3):
+        st = jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy()
+        assert np.array_equal(np.nonzero(st == 0)[0], bad)

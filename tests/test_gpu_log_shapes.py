@@ -123,3 +123,27 @@ def test_dense_list_in_chunks_random_lengths(gpu, jl, oracle):
         log[int(at)] ^= 0x10
     w = _check(jl, oracle, log)
     assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= 1
+
+
+@pytest.mark.parametrize("seed", [101, 202])
+def test_mixed_shapes_many_flips(gpu, jl, oracle, seed):
+    """~2 GB logs mixing short random-length records (runs of 1-3 and of
+    200-600 equal ones), DBBench-like 131-B stretches and long records
+    (500 B - 40 KB: dense blocks' deferred records and chunk rounds), 300 bit
+    flips; every live event against the oracle, checksum on and off (the
+    stress that found lc_dense's first_bad race, at this size)."""
+    rng = np.random.default_rng(seed)
+    m = (int(1.0 * (1 << 30)) // 120) // 3
+    kind = rng.random(m)
+    runs = np.where(kind < 0.01, rng.integers(200, 600, m), rng.integers(1, 4, m))
+    vals = np.where(kind > 0.999, rng.integers(500, 40000, m), rng.integers(0, 201, m))
+    vals = np.where((kind > 0.5) & (kind < 0.52), 131, vals)
+    log = _log(jl, gpu, np.repeat(vals, runs), seed=seed)
+    for at in rng.integers(0, log.numel(), 300):
+        log[int(at)] ^= 1 << int(rng.integers(0, 8))
+    host = log.cpu().numpy()
+    for checksum in (True, False):
+        ev, n = jl.log_verify_dev(log, checksum)
+        got = ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)
+        g, w = _live(got), _live(oracle.log_events(host, checksum=checksum))
+        assert g.shape == w.shape and np.array_equal(g, w), checksum
