@@ -1060,12 +1060,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 // end); key = w >> 8 = length | type << 16
                 const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
                 if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
-                    uint32_t m = 1;
                     if (key == pk) {
                         // it repeats the record before it: the run is measured from here
                         // (thread t: the candidate p + (t + 1) L) and joins that record's;
                         // one header read per record, no peek at the next (r4: records of
-                        // random lengths 6.9 -> 5.3 ms per GiB, tools/cliff_probe.py)
+                        // random lengths 6.9 -> 3.4 ms per GiB, tools/cliff_probe.py)
                         const uint32_t L = 7u + len, c = p + (t + 1u) * L;
                         const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
                         const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
@@ -1074,18 +1073,21 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                         if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
                         ld_sync();
                         const uint32_t f = uni(s_m[slot]);
-                        m = 1u + (f < kLDThreads ? f : kLDThreads);
+                        const uint32_t m = 1u + (f < kLDThreads ? f : kLDThreads);
                         trip++;
-                    } else {  // a new run (a block's leading fragment, a length change)
-                        if (t == 0) {
-                            run_a[nr] = p | (len << 16);
-                            run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
-                        }
-                        nr++;
+                        nev += m;
+                        p += m * L;
+                        continue;
                     }
+                    // a new run (a block's leading fragment, a length change)
+                    if (t == 0) {
+                        run_a[nr] = p | (len << 16);
+                        run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
+                    }
+                    nr++;
                     pk = key;
-                    nev += m;
-                    p += m * (7u + len);
+                    nev++;
+                    p += 7u + len;
                     continue;
                 }
                 // the block's end: the trailer (no event) or a record that stops the walk
