@@ -217,6 +217,8 @@ C5_LABELS = {
     "mixed_1b_100k": "C5 WAL verify, 2^17 x 32 KiB blocks, mixed 1 B-100 KiB records (fragmented), device-resident",
     "dbbench_131": "C5 WAL verify, 2^17 x 32 KiB blocks, DBBench-default 131-B records (16-B key + 100-B value, "
                    "DBBench.java:80; ~237 per block, every block dense), device-resident",
+    "random_0_200": "C5 WAL verify, 2^17 x 32 KiB blocks, 0-200-B records of random lengths (a WAL of variable "
+                    "small values; ~306 per block, every block dense, no runs), device-resident",
 }
 
 

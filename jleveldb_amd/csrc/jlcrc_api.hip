@@ -1248,7 +1248,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
                  o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
-                 o_end = o_nl + al(nb * 4);
+                 o_di = o_nl + al(nb * 4), o_dw = o_di + al(nb * 4), o_end = o_dw + al(nb * jlk::kDWMax * 2);
     JL_HIP(c.ws_lc.ensure(o_end));
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
     // The dense blocks' runs of events (lc_dense): no more runs than events, and
@@ -1289,6 +1289,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.dense_ctr = (uint32_t *)(ws + o_flag + 16);
     A.dense_list = (uint32_t *)(ws + o_dl);
     A.nlong = (uint32_t *)(ws + o_nl);
+    A.dw_info = (uint32_t *)(ws + o_di);
+    A.dw_off = (uint16_t *)(ws + o_dw);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
     A.stash_pool = pool;
@@ -1302,6 +1304,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // dense blocks: verified whole, exact counts, events stashed
     JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));  // lc_walk appends to the dense list at once; gv4 round counter
     JL_HIP(jlk::launch_lc_walk(A, st));
+    JL_HIP(jlk::launch_lc_dwalk(A, st));  // the dense blocks' headers, one lane per block
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:

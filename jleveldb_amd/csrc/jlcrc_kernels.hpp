@@ -178,6 +178,10 @@ struct LCArgs {
     LogEvent *ev;
     uint64_t ev_cap;
     const uint32_t *aux;
+    // lc_dwalk -> lc_dense: a dense block's first header offsets (kDWMax per block)
+    // and dw_info[b] = offsets | (where lc_dense's own walk resumes) << 16
+    uint16_t *dw_off;
+    uint32_t *dw_info;
 };
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st);
@@ -186,6 +190,15 @@ hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
+hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
+// lc_dwalk: header offsets kept per dense block; a run of kDWRun equal records
+// ends its walk (lc_dense's trips measure runs 257 records at a time)
+constexpr uint32_t kDWMax = 512;
+constexpr uint32_t kDWRun = 8;
+// lc_walk: a dense block whose last kDWProbe walked records are equal skips lc_dwalk
+// (dw_info = kDWUniform; an offset count | resume position << 16 never is)
+constexpr uint32_t kDWProbe = 4;
+constexpr uint32_t kDWUniform = 0xffffffffu;
 uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)

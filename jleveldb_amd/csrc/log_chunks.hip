@@ -285,6 +285,17 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A, uint32_t wg0) {
                 }
             }
             atomicAdd(&h[wv][kLCOver], 1u);
+            // a block whose last kDWProbe walked records are equal (DBBench's) is left
+            // to lc_dense's walk, whose trips measure such runs; the others are
+            // walked by lc_dwalk first
+            bool uniform = cnt >= kDWProbe + 1u;
+            const uint64_t s0 = cnt - 1u < kLCLdsSlots ? ls[threadIdx.x][cnt - 1u] : A.slots[b * kLCSlots + cnt - 1u];
+            for (uint32_t j = cnt - kDWProbe; uniform && j + 1u < cnt; j++) {
+                const uint64_t sj = j < kLCLdsSlots ? ls[threadIdx.x][j] : A.slots[b * kLCSlots + j];
+                uniform = (uint32_t)sj == (uint32_t)s0;
+            }
+            uniform = uniform && (((uint32_t)s0 >> 24) & 0xffu) == 1u;
+            A.dw_info[b] = uniform ? kDWUniform : 0u;
             cnt = kLCDense;
             listed = true;
         }
@@ -763,6 +774,60 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // A pass holds kLDRuns runs; a block of more (hundreds of short records of
 // changing lengths) takes several passes, their stash segments chained by a
 // link entry in the last slot of each.
+// lc_dwalk (r5): the headers of the dense blocks, one lane per block, read from
+// memory, before lc_dense.  lc_dense's own walk is one dependent chain per staged
+// block (4 per CU): blocks of short records of random lengths (no runs to measure
+// with its trips) cost ~1 K clocks per record on that chain, ~3 ms per GiB.  Here
+// every dense block of the log walks at once (8-byte header loads that hit the
+// block's lines in L2 after the first), and lc_dense only checks the crcs of the
+// records whose offsets it finds in dw_off.  The walk stops at kDWMax offsets,
+// at the first record that is not OK (lc_dense's walk decides it, as it decides
+// the rest of the block), and at a run of kDWRun equal records (lc_dense's trips
+// measure runs 257 records at a time: DBBench's blocks leave here after 8 hops).
+// Offsets are u16 (p < 32 KiB), eight per 16-B store.
+__global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.dense_ctr[0]) return;
+    const uint64_t b = A.dense_list[i], bs = b * 32768u;
+    if (A.dw_info[b] == kDWUniform) return;  // lc_walk: a run, lc_dense walks it
+    const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+    const uint8_t *blk = A.log + bs;
+    lc_v4 *out = (lc_v4 *)(A.dw_off + b * kDWMax);
+    uint32_t p = 0, n = 0, pk = ~0u, eq = 0;
+    bool go = true;
+    while (go) {
+        uint32_t q[4] = {0u, 0u, 0u, 0u};
+        const uint32_t n0 = n;
+#pragma unroll
+        for (uint32_t s = 0; s < 8u; s++) {
+            // (straight-line flags, no continue: an early `continue` here was
+            // miscompiled, the stored offset of a repeated record lost)
+            const uint32_t rem = blen - p;
+            bool st = !go || rem < 7u || n == kDWMax;
+            uint32_t key = 0, len = 0;
+            if (!st) {
+                // header bytes 3..6: [crc3][len lo][len hi][type]; key = length | type << 16
+                key = (uint32_t)(lc_header(blk + p, rem) >> 32) & 0xffffffu;
+                len = key & 0xffffu;
+                st = rem < 7u + len || key == 0u;  // not lc_decide's kind 1: lc_dense decides it
+            }
+            if (!st) {
+                const bool same = key == pk;
+                eq = same ? eq + 1u : 0u;
+                pk = key;
+                st = eq == kDWRun - 1u;  // a run: lc_dense measures it
+            }
+            const uint32_t put = st ? 0u : p << (16u * (s & 1u));
+            q[s >> 1] |= put;
+            n += st ? 0u : 1u;
+            p += st ? 0u : 7u + len;
+            go = go && !st;
+        }
+        if (n > n0) out[n0 / 8u] = lc_v4{q[0], q[1], q[2], q[3]};
+    }
+    A.dw_info[b] = n | (p << 16);
+}
+
 constexpr uint32_t kLDThreads = 256;
 __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
     return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
@@ -957,6 +1022,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t s_bad;           // header offset of the block's first failing record
     __shared__ unsigned long long s_seg;  // stash offset of the pass's segment (~0: did not fit)
     __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
+    __shared__ uint32_t doff[kDWMax / 2];  // lc_dwalk's header offsets of the block (u16 pairs)
     const uint32_t nd = uni(A.dense_ctr[0]);
     if (nd == 0) return;  // no dense block in the log
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -997,6 +1063,12 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     uint64_t bp = ~0ull;  // the previous block (its first_bad is written once its crc phase is done)
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
+    // lc_dwalk's offsets and info word of the block, fetched with its bytes
+    uint32_t pofs = 0, pinfo = 0;
+    if (b < A.n_blocks) {
+        pofs = ((const uint32_t *)(A.dw_off + b * kDWMax))[t];
+        pinfo = A.dw_info[b];
+    }
     unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
     uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
 #if JL_LD_PROF
@@ -1024,6 +1096,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
         }
         if (t < 4) dat[8192 + t] = 0;
+        doff[t] = pofs;
+        const uint32_t dinfo = uni(pinfo) == kDWUniform ? 0u : uni(pinfo);  // lc_dwalk: offsets | resume << 16
         if (t == 0) {
             // the previous block's failure, read after the barrier above: its crc
             // phase ends with no barrier when it was the block's last pass, so a
@@ -1041,11 +1115,17 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             grab = true;
         }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
+        if (bn < A.n_blocks) {
+            pofs = ((const uint32_t *)(A.dw_off + bn * kDWMax))[t];
+            pinfo = A.dw_info[bn];
+        }
         LD_T(tb);
 #if JL_LD_PRIO
         __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
 #endif
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
+        const uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each)
+        uint32_t dc = 0;                       // uniform: offsets taken
         uint64_t seg0 = ~0ull;      // uniform: the block's first segment (stash offset | entries << 48)
         uint64_t link = ~0ull;      // uniform: the previous segment's link slot
         bool fit = true, done = false;
@@ -1055,6 +1135,18 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             // ---- walk: up to kLDRuns runs from p
             uint32_t nr = 0, nev = 0;
             uint32_t pk = ~0u;  // uniform: the last run's key (below) when its records are OK
+            if (dc < dn) {  // lc_dwalk walked these: one run per record, thread t takes one
+                const uint32_t m = dn - dc < kLDRuns ? dn - dc : kLDRuns;
+                if (t < m) {
+                    const uint32_t o = (doff[(dc + t) >> 1] >> (16u * ((dc + t) & 1u))) & 0xffffu;
+                    const uint32_t w = lds32u(dat, o + 3u);
+                    run_a[t] = o | (w & 0xffff00u) << 8;
+                    run_b[t] = t | (w & 0xff000000u) >> 8 | (1u << 24);
+                }
+                nr = nev = m;  // m < kLDRuns: the last of them (the walk goes on in this pass)
+                dc += m;
+                if (dc == dn) p = dinfo >> 16;  // the block's rest: this walk from where lc_dwalk stopped
+            }
             while (nr < kLDRuns) {
                 // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
                 // end); key = w >> 8 = length | type << 16
@@ -1251,8 +1343,12 @@ extern "C" int jl_study_ld_prof(unsigned long long *out) {
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + kDWMax * 2 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
+}
+hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st) {
+    hipLaunchKernelGGL(lc_dwalk_kernel, dim3((A.n_blocks + 255u) / 256u), dim3(256), 0, st, A);
+    return hipGetLastError();
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
     hipLaunchKernelGGL(lc_dense_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);

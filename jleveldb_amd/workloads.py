@@ -16,7 +16,11 @@ C1_PAYLOAD = 12 + 1 + 1 + 16 + 2 + 1024  # WriteBatch header + tag + varint + 16
 # DBBench's default write (J/benchmark/DBBench.java:80 FLAGS_value_size = 100, 16-B keys):
 # one Put per WriteBatch = 12-B header + tag + varint + 16-B key + varint + 100-B value
 DBBENCH_PAYLOAD = 12 + 1 + 1 + 16 + 1 + 100
-C5_SETS = ("c1_1056", "mixed_1b_100k", "dbbench_131")
+# a WAL of variable small values: payloads of 0-200 B, uniform random lengths
+# (~306 records per 32 KiB block, every block dense, almost no two neighbours
+# equal: lc_dense's walk cannot join records into runs)
+RANDOM_MAX = 200
+C5_SETS = ("c1_1056", "mixed_1b_100k", "dbbench_131", "random_0_200")
 
 
 def c3_lengths(n: int = 1 << 20, seed: int = SEED) -> np.ndarray:
@@ -51,8 +55,14 @@ def c5_lengths(mixed, target: int = C5_LOG_BYTES, seed: int = SEED) -> np.ndarra
     bytes.  `mixed` names the set (C5_SETS; a bool picks the first two): C1-shaped
     records (1 056-B payloads), a mixed 1 B - 100 KiB set whose records fragment
     FIRST/MIDDLE/LAST across 32 KiB blocks, or DBBench-default records (131-B
-    payloads, ~237 per 32 KiB block: every block dense)."""
+    payloads, ~237 per 32 KiB block: every block dense), or 0-200-B payloads of
+    uniform random lengths (~306 per block, every block dense, runs of one)."""
     name = mixed if isinstance(mixed, str) else C5_SETS[1 if mixed else 0]
+    if name == "random_0_200":
+        rng = np.random.default_rng(seed + 13)
+        lens = rng.integers(0, RANDOM_MAX + 1, target // (RANDOM_MAX // 2 + 7) + 4096).astype(np.uint32)
+        keep = int(np.searchsorted(np.cumsum(_frag_bytes(lens)), target))
+        return lens[:keep]
     if name == "dbbench_131":
         return np.full(target // (DBBENCH_PAYLOAD + 7), DBBENCH_PAYLOAD, np.uint32)
     if name == "c1_1056":

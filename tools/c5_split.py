@@ -20,7 +20,7 @@ def short(name):
         return "scans"
     if "crc_gv4_kernel<5" in name:
         return "crc_gv4_kernel<LOG_CHUNK>"
-    for k in ("lc_walk", "lc_dense", "lc_build", "lc_setup", "lc_combine", "lc_apply"):
+    for k in ("lc_walk", "lc_dwalk", "lc_dense", "lc_build", "lc_setup", "lc_combine", "lc_apply"):
         if k + "_kernel" in name:
             return k
     return None
@@ -45,7 +45,9 @@ def main():
     for v in runs:
         if "crc_gv4_kernel<LOG_CHUNK>" not in v:
             continue
-        if v.get("lc_dense", 0) > 200:
+        if v.get("lc_dwalk", 0) > 100:
+            name = "random_0_200"
+        elif v.get("lc_dense", 0) > 200:
             name = "dbbench_131"
         elif v.get("lc_walk", 0) > 80:
             name = "c1_1056"
