@@ -101,11 +101,11 @@ const char *jl_version(void);
  *                            jl_table_verify: a call touching fewer bytes than
  *                            this runs on the calling thread's SSE4.2 path
  *                            (bit-identical; no device work; a device must still
- *                            be present); 0 = always the device.  Default 2 MiB,
- *                            the measured crossover of the per-call latencies
- *                            (one table)
+ *                            be present); 0 = always the device.  Default 4 MiB,
+ *                            the crossover of the per-call latencies on the
+ *                            round-end driver's boxes (one table)
  *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
- *                            default 8 MiB (the measured crossover; one ~4 MiB
+ *                            default 16 MiB (the driver's crossover; one ~4 MiB
  *                            WAL stays on the host)
  * Study builds only (make STUDY=1): JL_OPT_GV4_VARIANT (crc_gv4_kernel bound-study variants). */
 #define JL_OPT_GENERAL_PATH 1

@@ -36,7 +36,16 @@ class CopyPool {
         Job j{(char *)dst, (const char *)src, n, piece};
         {
             std::unique_lock<std::mutex> lk(mu_);
-            while ((int)th_.size() < threads - 1 && (int)th_.size() < 63) th_.emplace_back([this] { work(); });
+            // a thread that cannot be started (rlimit, a container's pid limit) must
+            // not throw through the C ABI: the copy goes on with the threads running
+            // (the caller alone if there are none), and no later call retries
+            while (!spawn_failed_ && (int)th_.size() < threads - 1 && (int)th_.size() < 63) {
+                try {
+                    th_.emplace_back([this] { work(); });
+                } catch (...) {
+                    spawn_failed_ = true;
+                }
+            }
             q_.push_back(&j);
             queued_.fetch_add(1);
         }
@@ -111,5 +120,6 @@ class CopyPool {
     std::atomic<int> queued_{0};  // jobs in q_ (read by spinning workers without the lock)
     std::vector<std::thread> th_;
     bool stop_ = false;
+    bool spawn_failed_ = false;  // guarded by mu_
 };
 }  // namespace jlhost

@@ -337,9 +337,9 @@ constexpr uint32_t kGvDealBatch = JL_GV4_DEAL_BATCH;
 #define JL_GV4_STATIC_DIV 4
 #endif
 constexpr uint32_t kGvStaticDiv = JL_GV4_STATIC_DIV;
-constexpr uint32_t kGvBatchDword = 7900;  // 16 slots {base, tag = batch + 1}: free in both gv4 images (zero)
+constexpr uint32_t kGvTagBits = 26, kGvTagMask = (1u << kGvTagBits) - 1u;  // reads <= kGvDealBatch < 64
+static_assert(kGvDealBatch < 64u, "a slot's read count takes 6 bits");
 constexpr uint32_t kGvNoRound = 0xffffffffu;  // >= any round count (< 2^31)
-constexpr uint32_t kGvDynDword = 7935;       // [0] the workgroup's counter, then 16 queues of 16 rounds
 
 // Prefetch cursor: walks the wave's rounds (seq(i), from the workgroup's counter) entry by entry.
 // L2W (study variant 7): every round's bytes are read from a 1 MiB window at the
@@ -373,6 +373,12 @@ struct GPF {
         if (JL_GV4_DEAL && deal && j >= J0) {  // batches of rounds from the device counter
             const uint32_t k = j - J0, X0 = J0 * G;
             const uint32_t b = k / DB, o = k - b * DB;
+            // slot s = {base, tag}: tag = (batch + 1) mod 2^kGvTagBits | rounds of that
+            // batch whose base was read << kGvTagBits.  A slot is reused by batch
+            // b + 16 only after all DB rounds of batch b read it: without that count
+            // (r4) a wave delayed between taking a round of batch b and reading its
+            // slot could find it overwritten by a batch 16 later (DB = 1 when the
+            // call has just over 64 G rounds): a hang on the tag, or a wrong base
             volatile uint32_t *slot = ctr + (kGvBatchDword - kGvDynDword);
             if (o == 0u) {  // opens batch b: take batch b + 1 (b = 0: batches 0 and 1)
                 const uint32_t n = b == 0u ? 2u * DB : DB;
@@ -385,12 +391,22 @@ struct GPF {
                         slot[1] = 1u;
                         g += DB;
                     }
-                    slot[2u * ((b + 1u) & 15u)] = g;  // base before tag: LDS writes of a wave land in order
-                    slot[2u * ((b + 1u) & 15u) + 1u] = b + 2u;
+                    const uint32_t s = 2u * ((b + 1u) & 15u);
+                    // its previous batch (b - 15) had all its rounds taken before this one
+                    // (the counter is monotonic), and each taker reads, then counts; its
+                    // tag is checked too (its opener may not have written it yet)
+                    if (b + 1u >= 16u)
+                        while (slot[s + 1u] != (((b - 14u) & kGvTagMask) | (DB << kGvTagBits)))
+                            __builtin_amdgcn_s_sleep(1);
+                    slot[s] = g;  // base before tag: LDS writes of a wave land in order
+                    slot[s + 1u] = (b + 2u) & kGvTagMask;
                 }
             }
-            while (uni(slot[2u * (b & 15u) + 1u]) != b + 1u) __builtin_amdgcn_s_sleep(1);
-            const uint64_t x = (uint64_t)X0 + uni(slot[2u * (b & 15u)]) + o;
+            const uint32_t s = 2u * (b & 15u);
+            while ((uni(slot[s + 1u]) & kGvTagMask) != ((b + 1u) & kGvTagMask)) __builtin_amdgcn_s_sleep(1);
+            const uint32_t base = uni(slot[s]);
+            if (lane0) atomicAdd((uint32_t *)(slot + s + 1u), 1u << kGvTagBits);  // read: LDS ops of a wave stay in order
+            const uint64_t x = (uint64_t)X0 + base + o;
             const uint32_t rr = x < R ? R - 1u - (uint32_t)x : kGvNoRound;
             Q[made & 15u] = rr;
             made++;

@@ -101,7 +101,7 @@ struct PinBuf {
 struct Slot {
     DevBuf d_in, d_desc, d_out;  // chunk bytes, packed descriptor arrays, results
     void *part[4] = {nullptr, nullptr, nullptr, nullptr};  // the descriptor arrays inside d_desc
-    PinBuf h_data, h_desc;
+    PinBuf h_data, h_desc, h_out;  // h_out: a log chunk's events on their way to the caller's array
     hipStream_t st = nullptr;
     hipEvent_t copied = nullptr, used = nullptr;
 };
@@ -140,6 +140,7 @@ struct Workspace {
             for (DevBuf *b : {&sl.d_in, &sl.d_desc, &sl.d_out}) b->release();
             sl.h_data.release();
             sl.h_desc.release();
+            sl.h_out.release();
             if (sl.copied) (void)hipEventDestroy(sl.copied);
             if (sl.used) (void)hipEventDestroy(sl.used);
             if (sl.st) (void)hipStreamDestroy(sl.st);
@@ -208,16 +209,19 @@ int get_ws(Workspace **out) {
 
 // Host-memory calls touching fewer bytes than these run on the calling thread's
 // SSE4.2 path (host_paths.cpp): below them the device round trip (copies,
-// launches, synchronisation) costs more than the CRC itself.  Measured per-call
-// latencies (bench.py "dispatch", r4j, pageable input, one caller; r4 staging
-// copies on a persistent thread pool and polled completion): a table of ~4.2 KB
-// blocks costs the device 105 us against the host's 74 at 1 MiB and 128 against
-// 146 at 2 MiB, so jleveldb's tables (>= 2 MiB, Options.java:208) go to the
-// device; a WAL of 1 056-B records costs the device 303 against 259 us at
-// 4 MiB and 469 against 515 at 8 MiB (its ~10 launches and the walk's dependent
-// header loads cost ~130 us at any size), so the reference's ~4 MiB WAL
-// (Options.java:203) stays on the host and logs from 8 MiB go to the device.
-constexpr int64_t kHostThresholdDefault = 2 << 20, kLogHostThresholdDefault = 8 << 20;
+// launches, synchronisation) costs more than the CRC itself.  The defaults are
+// the crossovers the round-end driver measured on fresh boxes (bench.py
+// "dispatch", BENCH_r03 / BENCH_r04, pageable input, one caller): a table of
+// ~4.2 KB blocks costs the device 156 us against the host's 146 at 2 MiB and 229
+// against 288 at 4 MiB; a WAL of 1 056-B records 591 against 514 us at 8 MiB and
+// 713 against 810 at 16 MiB.  Our own sessions measure the device ~20 % faster
+// at 2-16 MiB (r5f, a fresh box, dispatch first in its process: 122 vs 147 us
+// at 2 MiB, 486 vs 517 at 8 MiB; 64 MiB agrees everywhere), so the lower
+// crossovers (2 / 8 MiB) did not hold on the driver's boxes; at 4 / 16 MiB the
+// device is faster on every box measured.  jleveldb's 2 MiB tables
+// (Options.java:208) and ~4 MiB WALs (Options.java:203) therefore take the host
+// path; a compaction's input tables (jl_tables_verify) and larger logs the device.
+constexpr int64_t kHostThresholdDefault = 4 << 20, kLogHostThresholdDefault = 16 << 20;
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
 // batch takes and its tuning.  Defaults are the measured best; tests force the
@@ -810,6 +814,11 @@ int jl_init(int device) {
         std::vector<uint32_t> v4 = i < 3    ? jlmath::build_lds_image_v4(4 << i)
                                    : i == 3 ? jlmath::build_lds_image_gv4_rotated()
                                             : jlmath::build_lds_image_logchunk();
+        if (i >= 3) {  // the gv4 images: the round-dealing dwords must start zero (general_v4.hip)
+            for (uint32_t d = jlk::kGvBatchDword; d < jlk::kGvDynEnd; d++)
+                if ((d < jlk::kGvBatchDword + 32 || d >= jlk::kGvDynDword) && v4[d] != 0)
+                    return fail(JL_ERR_HIP, "init: a gv4 LDS image overlaps the round-dealing dwords");
+        }
         JL_HIP(hipMalloc(&c.d_img_v4[i], jlmath::kImageBytes));
         JL_HIP(hipMemcpy(c.d_img_v4[i], v4.data(), jlmath::kImageBytes, hipMemcpyHostToDevice));
     }
@@ -1259,12 +1268,13 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // kLDRuns + 1 entries per refill: refills <= entries / (pool - kLDRuns - 1) + grid.
     // A count-only call (no event array) stashes nothing: lc_dense skips the stores
     // of a pass that does not fit (stash_cap 0), and lc_build has no events to write.
+    // (a block's first pass may hold lc_dwalk's kDWMax records: segments of <= kDWMax + 1)
     const uint64_t need0 = d_events ? std::min<uint64_t>(cap, nb * (uint64_t)jlk::kLDMaxEv) : 0;
-    const uint64_t need = need0 + need0 / jlk::kLDRuns;
+    const uint64_t need = need0 + need0 / jlk::kLDRuns + (need0 ? nb : 0);
     const uint64_t grid = jlk::lc_dense_grid(ctx().cus);
     const uint64_t pool = need && nb >= 8 * grid ? jlk::kLDPool : 0;
-    const uint64_t stash_cap =
-        pool ? need + (need / (pool - jlk::kLDRuns - 1) + grid) * (jlk::kLDRuns + 1) + grid * pool : need;
+    const uint64_t seg = std::max<uint64_t>(jlk::kLDRuns, jlk::kDWMax) + 1;
+    const uint64_t stash_cap = pool ? need + (need / (pool - seg) + grid) * seg + grid * pool : need;
     JL_HIP(c.ws_stash.ensure(std::max<uint64_t>(stash_cap, 1) * 8));
     char *ws = (char *)c.ws_lc.p;
     jlk::LCArgs A;
@@ -1302,7 +1312,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
-    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));  // lc_walk appends to the dense list at once; gv4 round counter
+    // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
+    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
     JL_HIP(jlk::launch_lc_walk(A, st));
     JL_HIP(jlk::launch_lc_dwalk(A, st));  // the dense blocks' headers, one lane per block
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
@@ -1453,7 +1464,23 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     }
     HostSrc src(log, log_bytes);
     uint64_t total = 0;
-    const int rc = pipeline(
+    // A chunk's events leave by DMA into its slot's pinned h_out, and the host
+    // copies them into the caller's array while the next chunk runs (the copy
+    // pool).  r4 copied them with one hipMemcpyAsync into the caller's pageable
+    // array, which the runtime stages and the host waits for: on the DBBench set
+    // (0.5 GB of events per 4 GiB) the call ran at 38 GiB/s from pinned input.
+    struct Out {
+        Slot *sl = nullptr;
+        uint64_t at = 0, n = 0;
+    } pend;
+    auto flush = [&]() -> int {  // the pending chunk's events, once its D2H landed (`used`)
+        if (!pend.n) return JL_OK;
+        JL_HIP(hipEventSynchronize(pend.sl->used));
+        par_memcpy(events + pend.at, pend.sl->h_out.p, pend.n * sizeof(jl_log_event));
+        pend.n = 0;
+        return JL_OK;
+    };
+    int rc = pipeline(
         *w, (log_bytes + CH - 1) / CH,
         [&](uint64_t i, Slot &sl) { return slot_put_data(sl, src, i * CH, std::min(CH, log_bytes - i * CH)); },
         [&](uint64_t i, Slot &sl) -> int {
@@ -1464,11 +1491,16 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
                 return r;
             if (n && total + n <= cap) {  // past cap: keep counting for *n_events, copy nothing
                 JL_HIP(jlk::launch_event_rebase((jlk::LogEvent *)ev, n, i * CH, w->stream));
-                JL_HIP(hipMemcpyAsync(events + total, ev, n * sizeof(jl_log_event), hipMemcpyDeviceToHost, w->stream));
+                JL_HIP(sl.h_out.ensure(n * sizeof(jl_log_event)));
+                JL_HIP(hipMemcpyAsync(sl.h_out.p, ev, n * sizeof(jl_log_event), hipMemcpyDeviceToHost, w->stream));
             }
+            // the previous chunk's events (its slot's h_out is next written by chunk i + 1)
+            if (int r = flush()) return r;
+            if (n && total + n <= cap) pend = Out{&sl, total, n};
             total += n;
             return JL_OK;
         });
+    if (!rc) rc = flush();  // the pipeline drained: the last chunk's events landed
     *n_events = total;
     w->async_pending = false;  // the pipeline drained this thread's streams after any earlier async call
     if (rc) return rc;

@@ -166,7 +166,7 @@ struct LCArgs {
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
     uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range
     uint32_t *dense_list;  // n_blocks: the dense blocks (lc_walk appends, lc_dense takes them in chunks)
-    uint32_t *dense_ctr;   // [0] dense blocks listed, [1] list entries taken (zeroed before lc_walk)
+    uint32_t *dense_ctr;   // [0] dense blocks listed, [1] list entries taken, [2] gv4 deal, [3] lc_scan ids (zeroed before lc_walk)
     uint32_t *cap_flag;    // set when a capacity was exceeded
     uint64_t *result;      // [0] events, [1] dense blocks, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8
@@ -183,6 +183,11 @@ struct LCArgs {
     uint16_t *dw_off;
     uint32_t *dw_info;
 };
+// crc_gv4_kernel's round dealing state in its LDS image (general_v4.hip): dwords
+// [kGvBatchDword, +32) = 16 batch slots {base, tag | reads << 26}, [kGvDynDword,
+// kGvDynEnd) = the workgroup's counter and 16 queues of 16 rounds.  Both gv4
+// images leave them zero (checked when the images are built, jlcrc_api.hip).
+constexpr uint32_t kGvBatchDword = 7900, kGvDynDword = 7935, kGvDynEnd = kGvDynDword + 1 + 16 * 16;
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);

@@ -358,14 +358,22 @@ __device__ __forceinline__ uint32_t ls_block_excl(uint32_t v, uint32_t *wsum, ui
 }
 constexpr uint32_t kLSPer = kLSTile / 256u;  // values per thread
 static_assert(kLSTile % 256u == 0u, "kLSTile: a multiple of the workgroup");
+// Work ids come from a counter in dispatch order (dense_ctr[3], zeroed before
+// lc_walk), not from blockIdx.x: tile k's look-back spins on tiles k - 1 ..., so
+// it must not run before they have started, which a blockIdx order would only
+// assume of the hardware's dispatch (rocPRIM takes its tile ids the same way).
 __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
     __shared__ uint32_t buf[kLSTile];
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long s_pre;
+    __shared__ uint32_t s_id;
     const uint32_t t = threadIdx.x;
     const uint32_t tiles = (A.n_blocks + kLSTile) / kLSTile;  // n_blocks + 1 values
-    if (blockIdx.x < tiles) {
-        const uint64_t k = blockIdx.x, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
+    if (t == 0) s_id = atomicAdd(&A.dense_ctr[3], 1u);
+    __syncthreads();
+    const uint32_t id = s_id;
+    if (id < tiles) {
+        const uint64_t k = id, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
         for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
         __syncthreads();
         uint32_t v[kLSPer], s = 0;
@@ -406,7 +414,7 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
             if (base + j < n) A.start[base + j] = pre + buf[j];
         return;
     }
-    const uint32_t c = blockIdx.x - tiles;  // a hist row
+    const uint32_t c = id - tiles;  // a hist row
     const uint64_t nw = A.n_grp, row = (uint64_t)c * nw;
     uint32_t carry = 0;
     for (uint64_t g0 = 0; g0 < nw; g0 += kLSTile) {
@@ -603,6 +611,16 @@ __device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint
             const uint32_t cnt = r0 + lane < n && !link ? (uint32_t)(e >> 32) & 0xffffu : 0u;
             const uint32_t ex = lc_wave_excl_sum(cnt);
             const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)(ex + cnt), 63);
+            if (__builtin_amdgcn_ballot_w64(cnt > 1u) == 0ull) {
+                // runs of one record (lc_dwalk's blocks: records of random lengths):
+                // event ex is this lane's own run, no search
+                if (cnt) {
+                    const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32), len = lo >> 16;
+                    lc_event(A, ev0 + k0 + ex, b * 32768u + (lo & 0xffffu), len, (hi >> 16) & 0xffu, hi >> 24);
+                }
+                k0 += tot;
+                continue;
+            }
             for (uint32_t c0 = 0; c0 < tot; c0 += 64u) {
                 const uint32_t c = c0 + lane;
                 uint32_t o = 0;  // the last lane whose prefix is <= c: event c's run
@@ -759,8 +777,8 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 //          failing candidate (ballot, LDS min) ends the run: a run of equal
 //          records (DBBench's) is walked 257 headers per trip, one barrier each
 //          (J/db/LogReader.java:297-383, the reference's decisions in its order)
-//   crc    one thread per OK record, table lookups that never conflict (ld_zk:
-//          nibble tables, one copy each): the record's dwords end-aligned in
+//   crc    one thread per OK record, table lookups that never conflict (ld_map:
+//          5-bit tables, one copy each): the record's dwords end-aligned in
 //          groups of 4, four chains (position c of every group) stepping z^16,
 //          folded at the end with z^16 / z^12 / z^8 / z^4;
 //          the record's first bytes are seeded with W0 (the 4 bytes before it
@@ -836,43 +854,27 @@ __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // 
 __device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uint32_t c) {
     return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
 }
-// z^(4k)(x) ^ w from the nibble tables of z^(4k) (k = 1..4: 4, 8, 12, 16 zero
-// bytes; x: a chain's state XORed with its latest data dword):
-//   z^(4k)(x) = XOR_i N_k,i[(x >> 4i) & 15],  N_k,i[v] = z^(4k)(v << 4i).
-// A 16-entry table fills 16 distinct LDS banks, so two lanes either read the
-// same entry (broadcast) or different banks: nibble lookups never conflict, with
-// ONE copy of each table (r3's byte tables, one copy beside the staged block,
-// spent 58 % of the LDS cycles in bank conflicts, profiles/r3n_pmc_lc_dense.json).
-// The lookup address is v_perm_b32 of the nibbles spread one per byte, x4.
-__device__ __forceinline__ uint32_t ld_zk(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
-    const uint32_t lo = (x << 2) & 0x3c3c3c3cu, hi = (x >> 2) & 0x3c3c3c3cu;
-    uint32_t r[8];
-#pragma unroll
-    for (uint32_t i = 0; i < 8; i++) {
-        const uint32_t a = __builtin_amdgcn_perm(0u, i & 1u ? hi : lo, 0x0c0c0c00u | (i >> 1));
-        r[i] = *(const uint32_t *)((const char *)tab + 64u * i + a);
-    }
-    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], w));
-}
-// JL_LD_T5: the same maps from 5-bit tables, z^(4k)(x) = XOR_i F_k,i[(x >> 5i) & 31]
-// (i = 0..6, the last field 2 bits).  A 32-entry table fills the 32 banks a
-// ds_read_b32 lane group sees, so these never conflict either, and a dword costs
-// 7 lookups instead of 8 (2 VALU each for the address instead of 1 v_perm).
-#ifndef JL_LD_T5
-#define JL_LD_T5 1
-#endif
-constexpr uint32_t kLDTabDwords = JL_LD_T5 ? 7u * 32u : 128u;  // one map's tables
-__device__ __forceinline__ uint32_t ld_zk5(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
+// z^(4k)(x) ^ w from 5-bit tables (k = 1..4: 4, 8, 12, 16 zero bytes; x: a
+// chain's state XORed with its latest data dword):
+//   z^(4k)(x) = XOR_i F_k,i[(x >> 5i) & 31],  F_k,i[v] = z^(4k)(v << 5i), i = 0..6
+// (the last field 2 bits).  A 32-entry table fills the 32 banks a ds_read_b32
+// lane group sees, so two lanes either read the same entry (broadcast) or
+// different banks: these lookups never conflict, with ONE copy of each table
+// (r3's byte tables, one copy beside the staged block, spent 58 % of the LDS
+// cycles in bank conflicts, profiles/r3n_pmc_lc_dense.json).  7 lookups per
+// dword, 2 VALU each for the address.  Nibble tables (8 lookups) with their
+// addresses from one SDWA byte-select AND each (10 VALU per dword instead of 14)
+// were no faster (r5e, DBBench 1.296 vs 1.290 ms, random lengths 3.38 vs 3.32):
+// the crc phase is bound by the CU's LDS pipe, not by VALU issue, so lookups per
+// dword are what count.
+constexpr uint32_t kLDTabDwords = 7u * 32u;  // one map's tables
+__device__ __forceinline__ uint32_t ld_map(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
     uint32_t r[7];
     r[0] = *(const uint32_t *)((const char *)tab + ((x << 2) & 0x7cu));
 #pragma unroll
     for (uint32_t i = 1; i < 7; i++)
         r[i] = *(const uint32_t *)((const char *)tab + 128u * i + ((x >> (5u * i - 2u)) & 0x7cu));
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ w);
-}
-__device__ __forceinline__ uint32_t ld_map(const uint32_t *tab, uint32_t x, uint32_t w = 0u) {
-    if (JL_LD_T5) return ld_zk5(tab, x, w);
-    return ld_zk(tab, x, w);
 }
 // z(s) through T0 (one zero byte)
 __device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { return (s >> 8) ^ T0[s & 0xffu]; }
@@ -1032,11 +1034,10 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
     for (uint32_t w = t; w < 4u * kLDTabDwords; w += kLDThreads) {
-        // nibbles: N_k,i[v] = z^(4k)(v << 4i) at 128 (k-1) + 16 i + v; 5 bits: F_k,i[v] =
-        // z^(4k)(v << 5i) at 224 (k-1) + 32 i + v (i = 6: v < 4, the rest unused)
+        // F_k,i[v] = z^(4k)(v << 5i) at 224 (k-1) + 32 i + v (i = 6: v < 4, the rest unused)
         const uint32_t k = w / kLDTabDwords + 1u, e = w % kLDTabDwords;
-        const uint32_t i = JL_LD_T5 ? e >> 5 : e >> 4, v = JL_LD_T5 ? e & 31u : e & 15u;
-        uint32_t s = JL_LD_T5 ? (i * 5u < 32u ? v << (5u * i) : 0u) : v << (4u * i);
+        const uint32_t i = e >> 5, v = e & 31u;
+        uint32_t s = i * 5u < 32u ? v << (5u * i) : 0u;
         for (uint32_t z = 0; z < 4u * k; z++) s = ld_z1(t0, s);
         nt[w] = s;
     }
@@ -1097,6 +1098,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         if (t < 4) dat[8192 + t] = 0;
         doff[t] = pofs;
+        if (t <= 32u) run_b[t] = 0;  // the sort's bucket counts (lc_dwalk's pass)
         const uint32_t dinfo = uni(pinfo) == kDWUniform ? 0u : uni(pinfo);  // lc_dwalk: offsets | resume << 16
         if (t == 0) {
             // the previous block's failure, read after the barrier above: its crc
@@ -1129,134 +1131,177 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         uint64_t seg0 = ~0ull;      // uniform: the block's first segment (stash offset | entries << 48)
         uint64_t link = ~0ull;      // uniform: the previous segment's link slot
         bool fit = true, done = false;
+        // one OK record's crc (header at h, payload length len) against its stored crc
+        auto check = [&](uint32_t h, uint32_t len) {
+            const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
+            const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+            if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
+                const uint32_t k = atomicAdd(&A.nlong[b], 1u);  // < kLCSlots: >= 513 B each
+                A.slots[b * kLCSlots + k] = (uint64_t)h | ((uint64_t)len << 16) | ((uint64_t)lds32u(dat, h) << 32);
+                lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
+                return;
+            }
+            // the record's last dword is read whole: its 4 - tl bytes past the record
+            // (the next header's) enter the chains' result s linearly, as themselves
+            // (the last dword is chain 3's last word, XORed in unshifted), so s is
+            // compared with want ^ those bytes instead of masking the dword in the loop
+            const uint32_t gmask = tl ? ~((1u << (8u * tl)) - 1u) : 0u;
+            // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last dword
+            // was padded with 4 - tl zeros (tl = 0: the state): so u = z^-tl(stored
+            // state), tl = 0: z^-4 (inverse byte steps, ahead of the chains, so their
+            // dependent lookups overlap the chains'; one z^4 fold of 7 lookups less)
+            uint32_t want = ~unmask_crc(lds32u(dat, h));
+            for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(t0, want);
+            want ^= dat[a + nd - 1u] & gmask;
+            // the first dword, seeded (C_h folds in the seed dword before it)
+            const uint32_t d = dat[a];
+            uint32_t x0 = ~d;
+            if (hq) {
+                const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
+                x0 = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+            }
+            // four chains: the record's dwords end-aligned on groups of 4 (o zero
+            // dwords in front), chain c takes position c of every group and steps
+            // z^16; at the end chain c still owes z^(16 - 4c)
+            const uint32_t o = (4u - (nd & 3u)) & 3u, G = (nd + o) >> 2;
+            const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
+            uint32_t y[4];
+#pragma unroll
+            for (uint32_t c = 0; c < 4; c++) y[c] = c < o ? 0u : (c == o ? x0 : D[c]);
+            for (uint32_t g = 1; g < G; g++) {
+                uint32_t v[4];
+#pragma unroll
+                for (uint32_t c = 0; c < 4; c++) v[c] = D[4u * g + c];
+#pragma unroll
+                for (uint32_t c = 0; c < 4; c++) y[c] = ld_map(N16, y[c], v[c]);
+            }
+            const uint32_t sv = ld_map(N12, y[0]) ^ ld_map(N8, y[1]) ^ ld_map(N4, y[2]) ^ y[3];
+            if (sv != want) atomicMin(&s_bad, h);
+        };
+        auto doff16 = [&](uint32_t r) { return (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu; };
         while (!done) {
             // the block's failure so far: read before this pass's crc atomics can change it
             const bool crc = A.checksum && s_bad == kLCNone;
-            // ---- walk: up to kLDRuns runs from p
             uint32_t nr = 0, nev = 0;
-            uint32_t pk = ~0u;  // uniform: the last run's key (below) when its records are OK
-            if (dc < dn) {  // lc_dwalk walked these: one run per record, thread t takes one
-                const uint32_t m = dn - dc < kLDRuns ? dn - dc : kLDRuns;
-                if (t < m) {
-                    const uint32_t o = (doff[(dc + t) >> 1] >> (16u * ((dc + t) & 1u))) & 0xffffu;
-                    const uint32_t w = lds32u(dat, o + 3u);
-                    run_a[t] = o | (w & 0xffff00u) << 8;
-                    run_b[t] = t | (w & 0xff000000u) >> 8 | (1u << 24);
-                }
-                nr = nev = m;  // m < kLDRuns: the last of them (the walk goes on in this pass)
-                dc += m;
-                if (dc == dn) p = dinfo >> 16;  // the block's rest: this walk from where lc_dwalk stopped
-            }
-            while (nr < kLDRuns) {
-                // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
-                // end); key = w >> 8 = length | type << 16
-                const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
-                if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
-                    if (key == pk) {
-                        // it repeats the record before it: the run is measured from here
-                        // (thread t: the candidate p + (t + 1) L) and joins that record's;
-                        // one header read per record, no peek at the next (r4: records of
-                        // random lengths 6.9 -> 3.4 ms per GiB, tools/cliff_probe.py)
-                        const uint32_t L = 7u + len, c = p + (t + 1u) * L;
-                        const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
-                        const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
-                        const uint32_t slot = trip % 3u;
-                        if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
-                        if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
-                        ld_sync();
-                        const uint32_t f = uni(s_m[slot]);
-                        const uint32_t m = 1u + (f < kLDThreads ? f : kLDThreads);
-                        trip++;
-                        nev += m;
-                        p += m * L;
-                        continue;
+            const bool dpass = dc < dn;  // uniform
+            if (dpass) {
+                // ---- lc_dwalk's records (<= kDWMax, one run each) in ONE crc phase,
+                // sorted by their step count G (descending, a counting sort in
+                // run_b / run_a): each wave's 64 records then take about the same
+                // number of steps.  Random lengths in 256-record passes ran every wave
+                // to the longest of its 64 records, and a 2nd pass for the last ~50
+                // on one wave (r5d: lc_dense 1.98 ms per 4 GiB against 1.08 for
+                // DBBench's blocks).  Bucket 32 - G (G <= 32; long records, deferred
+                // to the rounds: bucket 32, last).
+                const uint32_t m = dn;
+                dc = dn;
+                p = dinfo >> 16;  // the block's rest: the walk below, from where lc_dwalk stopped
+                uint32_t bk[2] = {0u, 0u}, rk[2] = {0u, 0u};
+                if (crc) {
+#pragma unroll
+                    for (uint32_t i = 0; i < 2; i++) {
+                        const uint32_t r = t + 256u * i;
+                        if (r < m) {
+                            const uint32_t h = doff16(r), len = (lds32u(dat, h + 3u) >> 8) & 0xffffu;
+                            const uint32_t dw = ((h + 10u + len) >> 2) - ((h + 6u) >> 2);  // nd of check()
+                            bk[i] = dw > kLDLongDw ? 32u : 32u - ((dw + 3u) >> 2);
+                            rk[i] = atomicAdd(&run_b[bk[i]], 1u);
+                        }
                     }
-                    // a new run (a block's leading fragment, a length change)
-                    if (t == 0) {
-                        run_a[nr] = p | (len << 16);
-                        run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
+                    ld_sync();
+                    if (t < 64u) {  // bucket starts, after the 33 counts
+                        const uint32_t v = t <= 32u ? run_b[t] : 0u;
+                        const uint32_t ex = lc_wave_excl_sum(v);
+                        if (t <= 32u) run_b[64u + t] = ex;
                     }
-                    nr++;
-                    pk = key;
-                    nev++;
-                    p += 7u + len;
-                    continue;
-                }
-                // the block's end: the trailer (no event) or a record that stops the walk
-                const LCDecision d0 = lc_decide(rem, eof, rem >= 7u ? w : 0u);
-                if (d0.kind != 0u) {
-                    if (t == 0) {
-                        run_a[nr] = p | (d0.length << 16);
-                        run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
-                    }
-                    nr++;
-                    nev++;
-                }
-                done = true;
-                break;
-            }
-            ld_sync();  // the pass's runs are in LDS
+                    ld_sync();
+                    uint16_t *perm = (uint16_t *)run_a;  // sorted position -> record
+#pragma unroll
+                    for (uint32_t i = 0; i < 2; i++)
+                        if (t + 256u * i < m) perm[run_b[64u + bk[i]] + rk[i]] = (uint16_t)(t + 256u * i);
+                    ld_sync();
 #if JL_LD_PRIO
-            __builtin_amdgcn_s_setprio(0);
+                    __builtin_amdgcn_s_setprio(0);
 #endif
-            LD_T(tc);
-            // ---- crc: one thread per OK record (none once the block has a failure:
-            // the records after it are dropped whatever their crc)
-            if (crc) {
-                for (uint32_t r = t; r < nev; r += kLDThreads) {
-                    uint32_t j = 0;  // the run holding event r: the last with first <= r
-                    for (uint32_t s = kLDRuns / 2; s; s >>= 1)
-                        if (j + s < nr && (run_b[j + s] & 0xffffu) <= r) j += s;
-                    const uint32_t ra = run_a[j], rb = run_b[j];
-                    if ((rb >> 24) != 1u) continue;
-                    const uint32_t len = ra >> 16;
-                    const uint32_t h = (ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len);
-                    const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
-                    const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
-                    if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
-                        const uint32_t k = atomicAdd(&A.nlong[b], 1u);  // < kLCSlots: >= 513 B each
-                        A.slots[b * kLCSlots + k] = (uint64_t)h | ((uint64_t)len << 16) |
-                                                    ((uint64_t)lds32u(dat, h) << 32);
-                        lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
+                    for (uint32_t k = t; k < m; k += kLDThreads) {
+                        const uint32_t h = doff16(perm[k]);
+                        check(h, (lds32u(dat, h + 3u) >> 8) & 0xffffu);
+                    }
+                }
+                nr = nev = m;
+                // the walk from p ends at once, with no event (the block's trailer): no pass
+                done = blen - p < 7u && !(eof && blen - p > 0u);
+            } else {
+                // ---- walk: up to kLDRuns runs from p
+                uint32_t pk = ~0u;  // uniform: the last run's key (below) when its records are OK
+                while (nr < kLDRuns) {
+                    // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
+                    // end); key = w >> 8 = length | type << 16
+                    const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
+                    if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
+                        if (key == pk) {
+                            // it repeats the record before it: the run is measured from here
+                            // (thread t: the candidate p + (t + 1) L) and joins that record's;
+                            // one header read per record, no peek at the next (r4: records of
+                            // random lengths 6.9 -> 3.4 ms per GiB, tools/cliff_probe.py)
+                            const uint32_t L = 7u + len, c = p + (t + 1u) * L;
+                            const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
+                            const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
+                            const uint32_t slot = trip % 3u;
+                            if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
+                            if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
+                            ld_sync();
+                            const uint32_t f = uni(s_m[slot]);
+                            const uint32_t m = 1u + (f < kLDThreads ? f : kLDThreads);
+                            trip++;
+                            nev += m;
+                            p += m * L;
+                            continue;
+                        }
+                        // a new run (a block's leading fragment, a length change)
+                        if (t == 0) {
+                            run_a[nr] = p | (len << 16);
+                            run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
+                        }
+                        nr++;
+                        pk = key;
+                        nev++;
+                        p += 7u + len;
                         continue;
                     }
-                    const uint32_t tmask = tl ? (1u << (8u * tl)) - 1u : ~0u;
-                    // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last
-                    // dword was padded with 4 - tl zeros (tl = 0: the state): so u =
-                    // z^-tl(stored state), tl = 0: z^-4 (inverse byte steps, ahead of the
-                    // chains, so their dependent lookups overlap the chains'; one z^4 fold
-                    // of 7 lookups less per record)
-                    uint32_t want = ~unmask_crc(lds32u(dat, h));
-                    for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(t0, want);
-                    // the first dword, seeded (C_h folds in the seed dword before it)
-                    uint32_t d = dat[a];
-                    if (nd == 1u) d &= tmask;
-                    uint32_t x0 = ~d;
-                    if (hq) {
-                        const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
-                        x0 = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+                    // the block's end: the trailer (no event) or a record that stops the walk
+                    const LCDecision d0 = lc_decide(rem, eof, rem >= 7u ? w : 0u);
+                    if (d0.kind != 0u) {
+                        if (t == 0) {
+                            run_a[nr] = p | (d0.length << 16);
+                            run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
+                        }
+                        nr++;
+                        nev++;
                     }
-                    // four chains: the record's dwords end-aligned on groups of 4 (o
-                    // zero dwords in front), chain c takes position c of every group
-                    // and steps z^16; at the end chain c still owes z^(16 - 4c)
-                    const uint32_t o = (4u - (nd & 3u)) & 3u, G = (nd + o) >> 2;
-                    const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
-                    uint32_t y[4];
-#pragma unroll
-                    for (uint32_t c = 0; c < 4; c++) y[c] = c < o ? 0u : (c == o ? x0 : D[c]);
-                    if (G == 1u && o < 3u) y[3] &= tmask;
-                    for (uint32_t g = 1; g < G; g++) {
-                        uint32_t v[4];
-#pragma unroll
-                        for (uint32_t c = 0; c < 4; c++) v[c] = D[4u * g + c];
-                        if (g + 1u == G) v[3] &= tmask;
-#pragma unroll
-                        for (uint32_t c = 0; c < 4; c++) y[c] = ld_map(N16, y[c], v[c]);
+                    done = true;
+                    break;
+                }
+                ld_sync();  // the pass's runs are in LDS
+#if JL_LD_PRIO
+                __builtin_amdgcn_s_setprio(0);
+#endif
+                // ---- crc: one thread per OK record (none once the block has a failure:
+                // the records after it are dropped whatever their crc)
+                if (crc) {
+                    for (uint32_t r = t; r < nev; r += kLDThreads) {
+                        uint32_t j = 0;  // the run holding event r: the last with first <= r
+                        // steps from the largest power of two below nr (DBBench's blocks: 2-3 runs)
+                        for (uint32_t s = nr > 1u ? 1u << (31 - __builtin_clz(nr - 1u)) : 0u; s; s >>= 1)
+                            if (j + s < nr && (run_b[j + s] & 0xffffu) <= r) j += s;
+                        const uint32_t ra = run_a[j], rb = run_b[j];
+                        if ((rb >> 24) != 1u) continue;
+                        const uint32_t len = ra >> 16;
+                        check((ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len), len);
                     }
-                    const uint32_t s = ld_map(N12, y[0]) ^ ld_map(N8, y[1]) ^ ld_map(N4, y[2]) ^ y[3];
-                    if (s != want) atomicMin(&s_bad, h);
                 }
             }
+            LD_T(tc);
             LD_T(td);
             // ---- stash the pass's runs: one segment (+ a link slot when a pass follows).
             // The stash state is uniform (every thread tracks it); thread 0's atomic
@@ -1274,7 +1319,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)n);
                     ld_sync();
                     so = s_seg;
-                } else {  // a pass needs at most kLDRuns + 1 <= kLDPool entries
+                } else {  // a pass needs at most kDWMax + 1 <= kLDPool entries
                     if (pool_hi - pool_lo < n) {
                         if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
                         ld_sync();
@@ -1294,10 +1339,17 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 }
             }
             link = done || !fit ? ~0ull : so + nr;
-            if (t < nr && so != ~0ull) {
-                const uint32_t first = run_b[t] & 0xffffu;
-                const uint32_t next = t + 1u < nr ? run_b[t + 1u] & 0xffffu : nev;
-                A.stash[so + t] = ld_run_entry(run_a[t], run_b[t], next - first);
+            if (so != ~0ull) {
+                if (dpass) {  // record r: a run of one at its header, event r of the pass
+                    for (uint32_t r = t; r < nr; r += kLDThreads) {
+                        const uint32_t h = doff16(r), w = lds32u(dat, h + 3u);
+                        A.stash[so + r] = ld_run_entry(h | (w & 0xffff00u) << 8, r | (w & 0xff000000u) >> 8 | (1u << 24), 1u);
+                    }
+                } else if (t < nr) {
+                    const uint32_t first = run_b[t] & 0xffffu;
+                    const uint32_t next = t + 1u < nr ? run_b[t + 1u] & 0xffffu : nev;
+                    A.stash[so + t] = ld_run_entry(run_a[t], run_b[t], next - first);
+                }
             }
             total += nev;
 #if JL_LD_PRIO

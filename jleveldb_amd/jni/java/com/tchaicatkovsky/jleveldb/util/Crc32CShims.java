@@ -25,8 +25,10 @@ public final class Crc32CShims {
         if (rc != 0) throw new IllegalStateException("jlcrc: " + Crc32CNative.lastError());
         // the call-size dispatch (DESIGN.md §1.3): a table or log smaller than the
         // threshold is verified on the host's SSE4.2 path inside the engine; the
-        // defaults (the measured crossovers, DESIGN.md §1.3) send one >= 2 MiB table
-        // (maxFileSize) to the device and keep one ~4 MiB WAL (< 8 MiB) on the host
+        // defaults (the crossovers measured on fresh boxes, DESIGN.md §1.3: 4 MiB for
+        // tables, 16 MiB for logs) keep one 2 MiB table (maxFileSize) and one ~4 MiB
+        // WAL on the host and send a compaction's input tables (tablesVerify) and
+        // larger logs to the device
         setThreshold(Crc32CNative.OPT_HOST_THRESHOLD, "jlcrc.hostThreshold");
         setThreshold(Crc32CNative.OPT_LOG_HOST_THRESHOLD, "jlcrc.logHostThreshold");
     }

@@ -281,3 +281,25 @@ def test_gv4_table_verify_zipf_many_flips(gpu, jl):
     for _ in range(3):
         st = jl.table_verify_dev(d_f, d_off, d_size).cpu().numpy()
         assert np.array_equal(np.nonzero(st == 0)[0], bad)
+
+
+@pytest.mark.parametrize("n", [140_000, 200_000, 260_000])
+def test_gv4_batches_of_one_round(gpu, jl, oracle, n):
+    """17 500 - 32 500 rounds: just above 64 x the grid (256 workgroups), so the
+    device-counter batches hold ONE round each (general_v4.hip GPF::seq, DB = 1)
+    and batch slots are reused every 16 rounds: a slot's next batch waits until
+    every round of the one before has read its base.  Every CRC
+    against the oracle, five calls in a row."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    sizes = rng.integers(0, 900, n).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(sizes.astype(np.uint64) + 3)[:-1]
+    total = int(off[-1]) + int(sizes[-1]) + 3
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    d_a = torch.from_numpy(host).to(gpu)
+    d_off, d_len = to_dev(off.view(np.int64), gpu), to_dev(sizes.view(np.int32), gpu)
+    want = oracle.batch(host, off, sizes, threads=THREADS)
+    for _ in range(5):
+        assert np.array_equal(u32(jl.crc32c_batch_dev(d_a, d_off, d_len)), want)
