@@ -38,21 +38,10 @@
 
 #include "engine_device.hpp"
 
-#ifndef JL_RING_SLACK
-#define JL_RING_SLACK 2  // see general_v4.hip
-#endif
-
-// Study builds (-DJL_GV4_WAVETIME=1, tools/gv4_wavetime.py): every wave's start
-// and end time (s_memrealtime), read with jl_study_fx_wavetime.
-#ifndef JL_GV4_WAVETIME
-#define JL_GV4_WAVETIME 0
-#endif
 
 namespace jlk {
 
-#if JL_GV4_WAVETIME
-__device__ unsigned long long g_fx_wt[2 * 16384];
-#endif
+constexpr int kFxRingSlack = 2;  // ring waits vmcnt(P - 2): see general_v4.hip's JL_RING_SLACK
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
@@ -115,7 +104,7 @@ struct V4Wave {
     template <int K>
     __device__ __forceinline__ void step() {
         constexpr int SL = K % Gm::P;
-        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[SL]) : "n"(Gm::P - JL_RING_SLACK));
+        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(w[SL]) : "n"(Gm::P - kFxRingSlack));
         if (K == 0) {  // real XORs (zero is opaque): a plain copy here lets RA copy the ring slot before its wait
             x0 = s_init ^ w[SL].x;
             x1 = zero ^ w[SL].y;
@@ -145,107 +134,6 @@ struct V4Wave {
     }
 };
 
-#ifndef JL_FX_DYN
-#define JL_FX_DYN 0  // study: rounds dealt from an LDS counter (below); r4 A/B in DESIGN.md
-#endif
-#if JL_FX_DYN
-// Rounds (R blocks each) are dealt inside each workgroup from a counter in LDS
-// (r4): workgroup b owns rounds j G + b, j = 0, 1, ..., and each of its waves
-// takes the next j when it starts a round's prefetch, so a wave that runs faster
-// takes more rounds.  r3 gave every wave the same groups of 64 blocks; the 4
-// waves of a SIMD do not run at the same rate (issue goes to the oldest first),
-// so on C2 the waves of slots 0-3 ended at ~355 us, 4-7 at ~457, 8-11 at ~557 and
-// 12-15 at ~605 us of a 632-us launch, the last ~0.2 ms with ever fewer loads in
-// flight (tools/gv4_wavetime.py, profiles/r4k_wavetime.json).  A round's R
-// results leave as one store of 4 R bytes.  The counter is dword kFxDynDword of
-// the image (unused by the v4 image, zero when it is loaded).
-constexpr uint32_t kFxDynDword = 39936;
-constexpr uint32_t kFxNone = 0xffffffffu;
-template <int LPB, bool NT, int RING = 16, int THREADS = 1024>
-__global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__restrict__ img,
-                                                                 const uint8_t *__restrict__ data, uint64_t n_blocks,
-                                                                 uint32_t flags, uint32_t *__restrict__ out) {
-    using Gm = V4Geom<LPB, RING>;
-    __shared__ uint32_t lds[kImageBytes / 4];
-    load_image(lds, img);
-    const uint32_t lane = threadIdx.x & 63u;
-#if JL_GV4_WAVETIME
-    const uint64_t wid = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint64_t dbase = (uint64_t)(uintptr_t)data;
-    const uint32_t do_mask = flags & 1u;
-    const uint64_t rounds = (n_blocks + Gm::R - 1) / Gm::R;
-    uint32_t *ctr = lds + kFxDynDword;
-    // the workgroup's next round (kFxNone past its last), taken from the counter
-    // JL_FX_DYN 2: the workgroup owns a contiguous range of rounds instead (its
-    // waves stream one region, as the static groups do); 3: the same, each wave
-    // taking kFxSpan consecutive rounds at a time (a contiguous stretch per wave)
-    constexpr uint32_t kFxSpan = JL_FX_DYN == 3 ? 4u : 1u;
-    const uint64_t per = (rounds + gridDim.x - 1) / gridDim.x;
-    uint32_t span_next = 0, span_left = 0;  // uniform: the wave's next round of its stretch
-    auto take = [&]() -> uint32_t {
-        if (JL_FX_DYN == 3 && span_left) {
-            span_left--;
-            return span_next++;
-        }
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(ctr, 1u);
-        j = uni(j);
-        if (JL_FX_DYN >= 2) {
-            const uint64_t j0 = (uint64_t)j * kFxSpan, rr = (uint64_t)blockIdx.x * per + j0;
-            if (j0 >= per || rr >= rounds) return kFxNone;
-            const uint64_t lim = (per - j0 < kFxSpan ? per - j0 : kFxSpan);
-            const uint64_t n = rounds - rr < lim ? rounds - rr : lim;
-            span_next = (uint32_t)rr + 1u;
-            span_left = (uint32_t)n - 1u;
-            return (uint32_t)rr;
-        }
-        const uint64_t rr = (uint64_t)j * gridDim.x + blockIdx.x;
-        return rr < rounds ? (uint32_t)rr : kFxNone;
-    };
-    auto rsrc = [&](uint32_t rr) -> v4i {
-        if (rr == kFxNone) return make_rsrc(dbase, 0u);
-        const uint64_t b = (uint64_t)rr * Gm::R;
-        const uint64_t nb = n_blocks - b < (uint64_t)Gm::R ? n_blocks - b : (uint64_t)Gm::R;
-        return make_rsrc(dbase + b * 4096u, (uint32_t)(nb * 4096u));
-    };
-    uint32_t rc = take();  // the round the chains work on
-    if (rc == kFxNone) return;
-    uint32_t rn = take();  // the next one (its first P steps load during this round)
-
-    V4Wave<LPB, NT, RING> W(lds, lane);
-    W.voff = (lane / LPB) * 4096u + (lane % LPB) * 16u;
-    W.lc = 131072u | ((lane & 31u) << 2);
-    W.s_init = (lane % LPB == 0) ? 0xffffffffu : 0u;
-    W.cur = rsrc(rc);
-    W.nxt = rsrc(rn);
-    W.prime_all(std::make_integer_sequence<int, Gm::P>());
-
-    for (;;) {
-        W.round(std::make_integer_sequence<int, Gm::S>());
-        // rotate the prefetch resources: the next round's loads already use nxt
-        const uint32_t rd = rc;
-        rc = rn;
-        rn = rc == kFxNone ? kFxNone : take();
-        W.cur = W.nxt;
-        W.nxt = rsrc(rn);
-        uint32_t crc = W.finish();
-        if (do_mask) crc = mask_crc(crc);
-        const uint64_t blk = (uint64_t)rd * Gm::R + lane / LPB;
-        if (lane % LPB == 0 && blk < n_blocks) out[blk] = crc;
-        if (rc == kFxNone) break;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (zero-range) loads
-#if JL_GV4_WAVETIME
-    if (lane == 0 && wid < 16384u) {
-        g_fx_wt[2u * wid] = wt0;
-        g_fx_wt[2u * wid + 1u] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-}
-
-#else
 template <int LPB, bool NT, int RING = 16, int THREADS = 1024>
 __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__restrict__ img,
                                                                  const uint8_t *__restrict__ data, uint64_t n_blocks,
@@ -258,10 +146,6 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t g = uni64((uint64_t)blockIdx.x * (blockDim.x >> 6) + wave);  // group of 64 blocks
     if (g * 64u >= n_blocks) return;
-#if JL_GV4_WAVETIME
-    const uint64_t wid = g;
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     uint32_t *slot = lds + kV4SlotDword + wave * 64u;
     const uint64_t dbase = (uint64_t)(uintptr_t)data;
     const uint32_t do_mask = flags & 1u;
@@ -311,15 +195,7 @@ __global__ __launch_bounds__(THREADS) void crc_fixed4k_v4_kernel(const uint4 *__
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing (zero-range) loads
-#if JL_GV4_WAVETIME
-    if (lane == 0 && wid < 16384u) {
-        g_fx_wt[2u * wid] = wt0;
-        g_fx_wt[2u * wid + 1u] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
-
-#endif
 
 hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_blocks, uint32_t flags, uint32_t *out,
                              int grid, hipStream_t st) {
@@ -333,11 +209,3 @@ hipError_t launch_fixed4k_v4(const void *img, const uint8_t *data, uint64_t n_bl
 
 }  // namespace jlk
 
-#if JL_GV4_WAVETIME
-// study builds: per wave [start, end] of the last crc_fixed4k_v4_kernel launch (and clear them)
-extern "C" int jl_study_fx_wavetime(unsigned long long *out) {
-    static unsigned long long zero[2 * 16384];
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jlk::g_fx_wt), sizeof(zero)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(jlk::g_fx_wt), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-#endif

@@ -38,37 +38,14 @@ constexpr uint32_t kAuxZBDword = 5648 + 256 * 128;  // jlmath::kAuxZB
 struct LCGeom {
     uint32_t f, K, r, J;
 };
-#ifndef JL_LC_BIN_NO_D
-#define JL_LC_BIN_NO_D 0  // study: bins by K only (neighbouring records share rounds; epilogue tables per group)
-#endif
-__device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) {
-    return (K - 1u) * 16u + (JL_LC_BIN_NO_D ? 0u : (d & 15u));
-}
-#ifndef JL_LC_ILV
-#define JL_LC_ILV 0  // study: the rounds of one K j-major over its 16 d bins (see lc_round)
-#endif
-static_assert(!(JL_LC_ILV && JL_LC_BIN_NO_D), "JL_LC_ILV needs the d bins");
-// Round of the j-th round of bin (K, d).  Default: the bins' rounds in bin
-// order.  JL_LC_ILV: the rounds of one K interleaved over its 16 d bins (round j
-// of every bin, then round j + 1), so that neighbouring records of a stream of
-// similar lengths (which cycle through the d bins) sit in adjacent rounds, i.e.
-// on one XCD at about the same time, and their shared boundary lines come from
-// L2.  rs: kLCBins + 1 round starts (saturating: the total is clamped past the
-// descriptor capacity).
+__device__ __forceinline__ uint32_t lc_bin(uint32_t K, uint32_t d) { return (K - 1u) * 16u + (d & 15u); }
+// Round of the j-th round of bin (K, d): the bins' rounds in bin order (rs:
+// kLCBins + 1 round starts, saturating: the total is clamped past the descriptor
+// capacity).  r3 interleaved the rounds of one K over its 16 d bins so that
+// neighbouring records sit in adjacent rounds (their shared boundary lines from
+// L2): slower; on the branch study-r4-switches.
 __device__ __forceinline__ uint64_t lc_round(const uint32_t *rs, uint32_t K, uint32_t d, uint32_t j) {
-#if JL_LC_ILV
-    const uint32_t b0 = (K - 1u) * 16u, dd = d & 15u;
-    uint32_t pos = rs[b0];
-#pragma unroll
-    for (uint32_t e = 0; e < 16u; e++) {
-        const uint32_t a = rs[b0 + e], z = rs[b0 + e + 1u];
-        const uint32_t nr = z > a ? z - a : 0u;
-        pos += (nr < j ? nr : j) + (e < dd && nr > j ? 1u : 0u);
-    }
-    return pos;
-#else
     return (uint64_t)rs[lc_bin(K, d)] + j;
-#endif
 }
 __device__ __forceinline__ LCGeom lc_geom(uint64_t pa, uint32_t n) {
     LCGeom g;
@@ -113,61 +90,30 @@ typedef uint64_t __attribute__((aligned(1))) u64u;
 // Header bytes 0..6 at p ([crc 0..3][len lo][len hi][type]) as one 8-byte load
 // when 8 bytes are left in the block (one memory request on the walk's serial
 // chain), else two dword loads.
-// Cache policy of lc_walk's header hops: 1 = nt (the product), 0 = the default
-// policy, 2 = sc1, 3 = sc0 sc1, 4 = sc0 sc1 nt (study builds).  r3 same-box A/B
-// (tools/ab_lib.sh, 3 rounds): C5 1 056-B 1.034 -> 1.011 ms with nt (and with
-// sc0 sc1 nt), mixed and DBBench unchanged within noise; sc1 / sc0 sc1 alone no
-// change.  The walk's random header lines are not re-read soon (the rounds read
-// the records much later), so they should not displace L2-resident lines.
-#ifndef JL_LC_HDR_POLICY
-#define JL_LC_HDR_POLICY 1
-#endif
+// Cache policy of lc_walk's header hops: nt.  r3 same-box A/B (tools/ab_lib.sh, 3
+// rounds): C5 1 056-B 1.034 -> 1.011 ms with nt (and with sc0 sc1 nt), mixed and
+// DBBench unchanged within noise; sc1 / sc0 sc1 alone no change.  The walk's
+// random header lines are not re-read soon (the rounds read the records much
+// later), so they should not displace L2-resident lines.
 __device__ __forceinline__ uint64_t lc_header(const uint8_t *p, uint64_t rem) {
     if (rem >= 8) return *(const u64u *)p;
     return (uint64_t)ld_u32u(p) | ((uint64_t)(ld_u32u(p + 3) >> 8) << 32);
 }
-// the walk's hop load (lc_walk): lc_header's bytes with JL_LC_HDR_POLICY (an asm load,
-// waited for at once: the hop is a dependent chain anyway)
-// Study switch (0 in the product): non-temporal stores of the events / round
-// descriptors and loads of the stash (JL_NT_EV).  r3 same-box A/B
-// (tools/ab_lib.sh, C5 sets mixed / 1 056-B / DBBench, ms): product 0.82 /
-// 1.014 / 1.59, JL_NT_EV 0.825 / 1.035 / 1.587 (gv4 then reads its descriptors
-// from HBM); non-temporal staging loads in r3's lc_dense 0.826 / 1.02 / 1.62:
-// not kept.
-#ifndef JL_NT_EV
-#define JL_NT_EV 0
-#endif
+// Events, round descriptors and stash entries use the default cache policy: r3
+// same-box A/B (tools/ab_lib.sh, C5 sets mixed / 1 056-B / DBBench, ms): default
+// 0.82 / 1.014 / 1.59, non-temporal 0.825 / 1.035 / 1.587 (gv4 then reads its
+// descriptors from HBM).
 typedef uint32_t lc_v4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void lc_st16(void *p, lc_v4 v) {
-    if (JL_NT_EV) __builtin_nontemporal_store(v, (lc_v4 *)p);
-    else *(lc_v4 *)p = v;
-}
-__device__ __forceinline__ void lc_st8(uint64_t *p, uint64_t v) {
-    if (JL_NT_EV) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-__device__ __forceinline__ uint64_t lc_ld8(const uint64_t *p) {
-    if (JL_NT_EV) return __builtin_nontemporal_load(p);
-    return *p;
-}
+__device__ __forceinline__ void lc_st16(void *p, lc_v4 v) { *(lc_v4 *)p = v; }
+__device__ __forceinline__ uint64_t lc_ld8(const uint64_t *p) { return *p; }
+// the walk's hop load (lc_walk): lc_header's bytes as a non-temporal asm load,
+// waited for at once (the hop is a dependent chain anyway)
 __device__ __forceinline__ uint64_t lc_hop(const uint8_t *p, uint64_t rem) {
-#if JL_LC_HDR_POLICY
     if (rem >= 8) {
         uint64_t v;
-#if JL_LC_HDR_POLICY == 1
-#define JL_HP " nt"
-#elif JL_LC_HDR_POLICY == 2
-#define JL_HP " sc1"
-#elif JL_LC_HDR_POLICY == 3
-#define JL_HP " sc0 sc1"
-#else
-#define JL_HP " sc0 sc1 nt"
-#endif
-        asm volatile("global_load_dwordx2 %0, %1, off" JL_HP "\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-#undef JL_HP
+        asm volatile("global_load_dwordx2 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
         return v;
     }
-#endif
     return lc_header(p, rem);
 }
 
@@ -225,13 +171,13 @@ __device__ __forceinline__ void lc_hist_global(const LCArgs &A, uint64_t grp, co
 // makes every hop also wait for the store's acknowledgement (gfx9 counts stores
 // in vmcnt, and the compiler waits vmcnt(0) with a store outstanding).
 constexpr uint32_t kLCLdsSlots = 34;
-__global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A, uint32_t wg0) {
+__global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     __shared__ uint32_t h[4][kLCCounters];
     __shared__ uint64_t ls[256][kLCLdsSlots + 1];  // [thread][slot], padded: the write-back reads it in order
     const uint32_t wv = threadIdx.x >> 6;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t wg = wg0 + blockIdx.x;  // this launch's first workgroup (JL_LC_WALK_SPLIT)
+    const uint32_t wg = blockIdx.x;
     const uint64_t b = (uint64_t)wg * 256u + threadIdx.x;
     if (b == 0) {
         A.count[A.n_blocks] = 0;
@@ -470,19 +416,7 @@ __global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
         A.rstart[kLCBins] = over ? (uint32_t)A.round_cap : total;
         if (over) atomicOr(A.cap_flag, 1u);
     }
-#if JL_LC_ILV
-    uint64_t r = (uint32_t)__shfl((int)ex, (int)(lane & ~15u));  // the K's first round
-    {
-        const uint32_t j = cnt / 8u, dd = lane & 15u;
-#pragma unroll
-        for (uint32_t e = 0; e < 16u; e++) {
-            const uint32_t nr = (uint32_t)__shfl((int)rounds, (int)((lane & ~15u) + e));
-            r += (nr < j ? nr : j) + (e < dd && nr > j ? 1u : 0u);
-        }
-    }
-#else
     const uint64_t r = (uint64_t)ex + cnt / 8u;
-#endif
     if (cnt & 7u) {
         if (r < A.round_cap)
             for (uint32_t g = cnt & 7u; g < 8u; g++) A.desc[r * 8u + g].idx = kGNull;
@@ -574,12 +508,9 @@ __device__ __forceinline__ void lc_event(const LCArgs &A, uint64_t at, uint64_t 
 // ranges per bin come from the scan): one wave per block at a time, lane j =
 // event j (coalesced slot reads and event writes; the header offsets are the
 // prefix sums of 7 + length over the lanes).
-#ifndef JL_LC_BUILD_WAVES
-#define JL_LC_BUILD_WAVES 8
-#endif
 // 8 blocks per wave, all their loads issued first (r2: 8 waves x 8 blocks ran
 // lc_build 77 -> 63 us against 4 x 16, C5 ~3 % faster; 16 x 4 about the same)
-constexpr uint32_t kLCBuildWaves = JL_LC_BUILD_WAVES;
+constexpr uint32_t kLCBuildWaves = 8;
 
 // A dense block's events from its runs (lc_dense's stash segments): a wave takes
 // 64 runs at a time (lane = run: its count, exclusive prefix over the lanes),
@@ -893,9 +824,6 @@ __device__ __forceinline__ uint32_t ld_zi1(const uint32_t *Ti, uint32_t s) { ret
 // of walk each) dealt 8 at a time left its workgroups ending 2.26 .. 3.24 ms
 // (profiles/r4bc_walk_variants_ldprof.json)
 constexpr uint32_t kLDChunk = 8;
-#ifndef JL_LD_CHUNK_ADAPT
-#define JL_LD_CHUNK_ADAPT 1
-#endif
 __device__ __forceinline__ uint32_t ld_chunk(uint32_t nd) {
     const uint32_t c = nd / (16u * gridDim.x);
     return c < 1u ? 1u : (c > kLDChunk ? kLDChunk : c);
@@ -985,24 +913,10 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
     return (uint64_t)ra | ((uint64_t)cnt << 32) | ((uint64_t)(rb >> 16) << 48);
 }
 
-// Study builds (-DJL_LD_PROF=1, tools/ld_prof.py): per workgroup, shader clocks
-// (s_memtime of thread 0) spent in each phase over all its blocks — [0] waiting
-// for / storing the staged block, [1] walk, [2] crc, [3] stash, [4] blocks —
-// and its start / end time (s_memrealtime, 100 MHz, one clock for the chip).
-#ifndef JL_LD_PROF
-#define JL_LD_PROF 0
-#endif
-// The walk and a block's staging (2; 1: the walk only) at a higher wave priority than the crc phase:
-// its dependent LDS trips then queue behind fewer of the other workgroups' lookups
-#ifndef JL_LD_PRIO
-#define JL_LD_PRIO 2
-#endif
-#if JL_LD_PROF
-__device__ unsigned long long g_ld_prof[4096 * 8];
-#define LD_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
-#else
-#define LD_T(v)
-#endif
+// The walk and a block's staging run at a higher wave priority than the crc
+// phase (s_setprio 2, then 0): their dependent LDS trips then queue behind fewer
+// of the other workgroups' lookups (r4: DBBench 1.371 -> 1.348 ms).  (The per-phase
+// clock study, JL_LD_PROF / tools/ld_prof.py, lives on the branch study-r4-switches.)
 
 // A record of more than kLDLongDw dwords in a dense block is not checked by one
 // thread here: a 31 KiB record after a few short ones held its workgroup ~170 us
@@ -1029,7 +943,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     if (nd == 0) return;  // no dense block in the log
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0)
-        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], JL_LD_CHUNK_ADAPT ? ld_chunk(nd) : kLDChunk);
+        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], ld_chunk(nd));
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
@@ -1056,7 +970,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     const uint32_t C1 = ld_map(N4, W0 << 8), C2 = ld_map(N4, W0 << 16), C3 = ld_map(N4, W0 << 24);
     LDSched sch;
     sch.nd = nd;
-    sch.ch = JL_LD_CHUNK_ADAPT ? ld_chunk(nd) : kLDChunk;
+    sch.ch = ld_chunk(nd);
     sch.init(A, s_c[0], s_c[1]);
     bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
     uint32_t grabbed = 0;
@@ -1072,18 +986,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     }
     unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
     uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
-#if JL_LD_PROF
-    uint64_t acc[5] = {0, 0, 0, 0, 0};
-    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     while (b < A.n_blocks) {
-        LD_T(ta);
         const uint64_t bs = b * 32768u;
         const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
         const bool eof = blen < 32768u;
-#if JL_LD_PRIO >= 2
         __builtin_amdgcn_s_setprio(2);
-#endif
         ld_sync();  // the previous block's readers of dat / runs / s_* are done
         if (ld_vec(A, b)) {
             pre.store(dat, t);
@@ -1121,10 +1028,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             pofs = ((const uint32_t *)(A.dw_off + bn * kDWMax))[t];
             pinfo = A.dw_info[bn];
         }
-        LD_T(tb);
-#if JL_LD_PRIO
         __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
-#endif
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
         const uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each)
         uint32_t dc = 0;                       // uniform: offsets taken
@@ -1220,9 +1124,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     for (uint32_t i = 0; i < 2; i++)
                         if (t + 256u * i < m) perm[run_b[64u + bk[i]] + rk[i]] = (uint16_t)(t + 256u * i);
                     ld_sync();
-#if JL_LD_PRIO
                     __builtin_amdgcn_s_setprio(0);
-#endif
                     for (uint32_t k = t; k < m; k += kLDThreads) {
                         const uint32_t h = doff16(perm[k]);
                         check(h, (lds32u(dat, h + 3u) >> 8) & 0xffffu);
@@ -1283,9 +1185,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     break;
                 }
                 ld_sync();  // the pass's runs are in LDS
-#if JL_LD_PRIO
                 __builtin_amdgcn_s_setprio(0);
-#endif
                 // ---- crc: one thread per OK record (none once the block has a failure:
                 // the records after it are dropped whatever their crc)
                 if (crc) {
@@ -1301,8 +1201,6 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                     }
                 }
             }
-            LD_T(tc);
-            LD_T(td);
             // ---- stash the pass's runs: one segment (+ a link slot when a pass follows).
             // The stash state is uniform (every thread tracks it); thread 0's atomic
             // reaches the others through LDS only when a pool is refilled (every ~69
@@ -1352,21 +1250,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 }
             }
             total += nev;
-#if JL_LD_PRIO
-            if (!done) __builtin_amdgcn_s_setprio(2);
-#endif
-            if (!done) ld_sync();  // the next pass's walk rewrites the runs
-#if JL_LD_PROF
-            LD_T(te);
-            acc[1] += tc - tb;
-            acc[2] += td - tc;
-            acc[3] += te - td;
-#endif
+            if (!done) {
+                __builtin_amdgcn_s_setprio(2);
+                ld_sync();  // the next pass's walk rewrites the runs
+            }
         }
-#if JL_LD_PROF
-        acc[0] += tb - ta;
-        acc[4] += 1;
-#endif
         if (t == 0) {
             A.count[b] = total;
             A.dense_off[b] = fit ? seg0 : ~0ull;
@@ -1375,23 +1263,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     }
     ld_sync();  // the last block's crc phase is done
     if (t == 0 && bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
-#if JL_LD_PROF
-    if (t == 0 && blockIdx.x < 4096u) {
-        for (int i = 0; i < 5; i++) g_ld_prof[8u * blockIdx.x + i] = acc[i];
-        g_ld_prof[8u * blockIdx.x + 5] = rt0;
-        g_ld_prof[8u * blockIdx.x + 6] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
-
-#if JL_LD_PROF
-// study builds: read (and clear) lc_dense's per-workgroup phase clocks (see g_ld_prof)
-extern "C" int jl_study_ld_prof(unsigned long long *out) {
-    static unsigned long long zero[4096 * 8];
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ld_prof), sizeof(zero)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_ld_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
@@ -1407,20 +1279,9 @@ hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Study (JL_LC_WALK_SPLIT = S > 1): the walk as S launches over consecutive block
-// ranges, fewer hop chains in flight over a smaller part of the log at a time
-#ifndef JL_LC_WALK_SPLIT
-#define JL_LC_WALK_SPLIT 1
-#endif
 hipError_t launch_lc_walk(const LCArgs &A, hipStream_t st) {
-    const uint32_t W = (A.n_grp + 3) / 4, S = JL_LC_WALK_SPLIT;
-    if (S > 1 && W >= 64u * S) {
-        const uint32_t per = (W + S - 1) / S;
-        for (uint32_t w0 = 0; w0 < W; w0 += per)
-            hipLaunchKernelGGL(lc_walk_kernel, dim3(W - w0 < per ? W - w0 : per), dim3(256), 0, st, A, w0);
-        return hipGetLastError();
-    }
-    hipLaunchKernelGGL(lc_walk_kernel, dim3(W), dim3(256), 0, st, A, 0u);
+    const uint32_t W = (A.n_grp + 3) / 4;
+    hipLaunchKernelGGL(lc_walk_kernel, dim3(W), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_scan(const LCArgs &A, hipStream_t st) {
