@@ -1315,7 +1315,11 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
     JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
     JL_HIP(jlk::launch_lc_walk(A, st));
-    JL_HIP(jlk::launch_lc_dwalk(A, st));  // the dense blocks' headers, one lane per block
+    // the dense blocks' headers (lc_dwalk, one lane per block), then their crcs
+    // (lc_dense).  r5 measured lc_dwalk of half the list on a second stream beside
+    // lc_dense of the other half: random lengths 2.64 -> 2.47 ms, but every other
+    // set 3-5 % slower (the cross-stream waits and the extra launches, ~40 us)
+    JL_HIP(jlk::launch_lc_dwalk(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:

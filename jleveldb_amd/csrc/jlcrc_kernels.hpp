@@ -124,7 +124,7 @@ constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk r
 // the rounds, and lc_dense verifies it whole from a copy staged in LDS, writes
 // its exact event count and stashes its events (lc_build places them)
 constexpr uint32_t kLCSlots = 64;
-constexpr uint32_t kLCProbe = 8;
+constexpr uint32_t kLCProbe = 4;
 constexpr uint32_t kLCDense = 0xffffffffu;  // count[b] of a dense block until lc_dense counts it
 constexpr uint32_t kLDMaxEv = 4688;         // >= events (and runs) of one 32 KiB block (one per 7 bytes)
 constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
@@ -201,9 +201,9 @@ hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
 constexpr uint32_t kDWMax = 512;
 constexpr uint32_t kDWRun = 8;
 // lc_walk: a dense block whose last kDWProbe walked records are equal skips lc_dwalk
-// (dw_info = kDWUniform; an offset count | resume position << 16 never is)
-constexpr uint32_t kDWProbe = 4;
-constexpr uint32_t kDWUniform = 0xffffffffu;
+// (its dense_list entry carries kDWUniform; block indices are < 2^31)
+constexpr uint32_t kDWProbe = 3;
+constexpr uint32_t kDWUniform = 0x80000000u;
 uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)

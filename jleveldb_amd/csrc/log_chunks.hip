@@ -185,7 +185,8 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
         *A.stash_ctr = 0;
     }
     uint32_t cnt = 0;
-    bool listed = false;  // a dense block: appended to lc_dense's list below
+    bool listed = false;   // a dense block: appended to lc_dense's list below
+    bool uniform = false;  // ... whose last walked records are equal (kDWUniform in its list entry)
     if (b < (A.n_blocks + kLSTile) / kLSTile) A.tstat[b] = 0;  // lc_scan's look-back statuses
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
@@ -234,14 +235,13 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
             // a block whose last kDWProbe walked records are equal (DBBench's) is left
             // to lc_dense's walk, whose trips measure such runs; the others are
             // walked by lc_dwalk first
-            bool uniform = cnt >= kDWProbe + 1u;
+            uniform = cnt >= kDWProbe + 1u;
             const uint64_t s0 = cnt - 1u < kLCLdsSlots ? ls[threadIdx.x][cnt - 1u] : A.slots[b * kLCSlots + cnt - 1u];
             for (uint32_t j = cnt - kDWProbe; uniform && j + 1u < cnt; j++) {
                 const uint64_t sj = j < kLCLdsSlots ? ls[threadIdx.x][j] : A.slots[b * kLCSlots + j];
                 uniform = (uint32_t)sj == (uint32_t)s0;
             }
             uniform = uniform && (((uint32_t)s0 >> 24) & 0xffu) == 1u;
-            A.dw_info[b] = uniform ? kDWUniform : 0u;
             cnt = kLCDense;
             listed = true;
         }
@@ -261,7 +261,9 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     __syncthreads();
     if (threadIdx.x == 0 && s_dn) s_db = atomicAdd(&A.dense_ctr[0], s_dn);
     __syncthreads();
-    if (listed) A.dense_list[s_db + woff + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] = (uint32_t)b;
+    if (listed)
+        A.dense_list[s_db + woff + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] =
+            (uint32_t)b | (uniform ? kDWUniform : 0u);
     // the LDS slots out, the workgroup's 256 blocks together: consecutive threads
     // store a block's consecutive slots (a run of kLCLdsSlots x 8 B per block; one
     // thread per block writing its own slots touched 64 lines per store, 33 us of
@@ -737,8 +739,9 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 __global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= A.dense_ctr[0]) return;
-    const uint64_t b = A.dense_list[i], bs = b * 32768u;
-    if (A.dw_info[b] == kDWUniform) return;  // lc_walk: a run, lc_dense walks it
+    const uint32_t e = A.dense_list[i];
+    if (e & kDWUniform) return;  // lc_walk: a run, lc_dense walks it (and reads no dw_info)
+    const uint64_t b = e, bs = b * 32768u;
     const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
     const uint8_t *blk = A.log + bs;
     lc_v4 *out = (lc_v4 *)(A.dw_off + b * kDWMax);
@@ -940,10 +943,11 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
     __shared__ uint32_t doff[kDWMax / 2];  // lc_dwalk's header offsets of the block (u16 pairs)
     const uint32_t nd = uni(A.dense_ctr[0]);
+    uint32_t *const ctr = &A.dense_ctr[1];  // list entries taken
     if (nd == 0) return;  // no dense block in the log
     const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
     if (t == 0)
-        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(&A.dense_ctr[1], ld_chunk(nd));
+        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(ctr, ld_chunk(nd));
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
@@ -974,13 +978,14 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     sch.init(A, s_c[0], s_c[1]);
     bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
     uint32_t grabbed = 0;
-    uint64_t b = sch.next(A, s_c[2], &moved);
+    // list entries: block | kDWUniform when lc_walk left the block to this walk alone
+    uint64_t be = sch.next(A, s_c[2], &moved), b = be & ~(uint64_t)kDWUniform;
     uint64_t bp = ~0ull;  // the previous block (its first_bad is written once its crc phase is done)
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
     // lc_dwalk's offsets and info word of the block, fetched with its bytes
     uint32_t pofs = 0, pinfo = 0;
-    if (b < A.n_blocks) {
+    if (b < A.n_blocks && !(be & kDWUniform)) {
         pofs = ((const uint32_t *)(A.dw_off + b * kDWMax))[t];
         pinfo = A.dw_info[b];
     }
@@ -1006,7 +1011,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         if (t < 4) dat[8192 + t] = 0;
         doff[t] = pofs;
         if (t <= 32u) run_b[t] = 0;  // the sort's bucket counts (lc_dwalk's pass)
-        const uint32_t dinfo = uni(pinfo) == kDWUniform ? 0u : uni(pinfo);  // lc_dwalk: offsets | resume << 16
+        const uint32_t dinfo = uni(pinfo);  // lc_dwalk: offsets | resume << 16 (0: none)
         if (t == 0) {
             // the previous block's failure, read after the barrier above: its crc
             // phase ends with no barrier when it was the block's last pass, so a
@@ -1018,13 +1023,14 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         bp = b;
         ld_sync();
-        const uint64_t bn = sch.next(A, s_c[2], &moved);  // its bytes load during this block's work
+        const uint64_t bne = sch.next(A, s_c[2], &moved), bn = bne & ~(uint64_t)kDWUniform;  // loads during this block
         if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
-            grabbed = atomicAdd(&A.dense_ctr[1], sch.ch);
+            grabbed = atomicAdd(ctr, sch.ch);
             grab = true;
         }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
-        if (bn < A.n_blocks) {
+        pofs = pinfo = 0;
+        if (bn < A.n_blocks && !(bne & kDWUniform)) {
             pofs = ((const uint32_t *)(A.dw_off + bn * kDWMax))[t];
             pinfo = A.dw_info[bn];
         }
