@@ -287,18 +287,26 @@ def secondary_c5(dev, stream, steps, warmup, which="c1_1056", cpu=True, host_cop
     del log, events
     torch.cuda.empty_cache()
     hn = host.numpy()
-    jl.log_verify(hn)
-    t0 = time.perf_counter()
-    hev = jl.log_verify(hn)
-    el = time.perf_counter() - t0
-    res["copy_inclusive_GiB_per_s"] = round(nb / el / GIB, 2)  # pinned source, 64 MiB chunks double-buffered
+    # the event array is allocated and touched once and reused (a caller's buffer):
+    # a fresh multi-GB array per call times the kernel's page faults on its first
+    # writes, not the engine (r4: pinned 38 < pageable 47 GiB/s on the DBBench set)
+    out = np.zeros(int(plan["len"].size) + 64, dtype=jl.LOG_EVENT_DTYPE)
+    jl.log_verify(hn, out=out)
+
+    def median_rate(src, k=3):
+        ts = []
+        for _ in range(k):
+            t0 = time.perf_counter()
+            jl.log_verify(src, out=out)
+            ts.append(time.perf_counter() - t0)
+        return round(nb / float(np.median(ts)) / GIB, 2)
+
+    res["copy_inclusive_GiB_per_s"] = median_rate(hn)  # pinned source, 64 MiB chunks double-buffered; median of 3
+    hev = jl.log_verify(hn, out=out)
     res["copy_inclusive_records_ok"] = int((hev["kind"] == jl.LOG_OK).sum())
     del host, hev
-    pageable = hn.copy()  # the same log in pageable memory (an mmap'd file's case): pinned for the call
-    t0 = time.perf_counter()
-    hev = jl.log_verify(pageable)
-    res["copy_inclusive_pageable_GiB_per_s"] = round(nb / (time.perf_counter() - t0) / GIB, 2)
-    del hev
+    pageable = hn.copy()  # the same log in pageable memory (an mmap'd file's case): pinned for each call
+    res["copy_inclusive_pageable_GiB_per_s"] = median_rate(pageable)
     hn = pageable
     if cpu:  # the oracle's readPhysicalRecord walk + crc on the log's first 1 GiB: one thread, and
         # all threads over block-aligned pieces (readPhysicalRecord decides within a 32 KiB block)

@@ -449,12 +449,18 @@ def log_emit_dev(src, plan, out=None, stream=None):
     return out[:nb]
 
 
-def log_verify(log, checksum: bool = True) -> np.ndarray:
+def log_verify(log, checksum: bool = True, out=None) -> np.ndarray:
     """Device verification of a host log image (numpy / bytes / CPU tensor) ->
-    physical-record events (LOG_EVENT_DTYPE).  `checksum`: bool or a LOG_* mode."""
+    physical-record events (LOG_EVENT_DTYPE).  `checksum`: bool or a LOG_* mode.
+    `out`: an event array (LOG_EVENT_DTYPE) to fill, reused across calls; its
+    size is the capacity (a log has at most size / 7 + 2 physical records)."""
     ptr, size, _keep = _host_bytes(log)
-    cap = size // 7 + 2
-    ev = np.zeros(cap, dtype=LOG_EVENT_DTYPE)
+    if out is None:
+        cap = size // 7 + 2
+        ev = np.zeros(cap, dtype=LOG_EVENT_DTYPE)
+    else:
+        assert out.dtype == LOG_EVENT_DTYPE and out.flags.c_contiguous
+        ev, cap = out, out.size
     n = ctypes.c_uint64(0)
     _check(lib().jl_log_verify(ptr if size else None, size, int(checksum), ev.ctypes.data, cap,
                                ctypes.byref(n)), "jl_log_verify")

@@ -317,9 +317,13 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
     __shared__ uint32_t s_id;
     const uint32_t t = threadIdx.x;
     const uint32_t tiles = (A.n_blocks + kLSTile) / kLSTile;  // n_blocks + 1 values
-    if (t == 0) s_id = atomicAdd(&A.dense_ctr[3], 1u);
-    __syncthreads();
-    const uint32_t id = s_id;
+    // the hist rows (independent) are workgroups [0, kLCCounters); only the tiles
+    // take ordered ids (one atomic per tile, not per workgroup)
+    if (blockIdx.x >= kLCCounters) {
+        if (t == 0) s_id = atomicAdd(&A.dense_ctr[3], 1u);
+        __syncthreads();
+    }
+    const uint32_t id = blockIdx.x >= kLCCounters ? s_id : tiles + blockIdx.x;
     if (id < tiles) {
         const uint64_t k = id, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
         for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
@@ -788,7 +792,7 @@ __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // 
 __device__ __forceinline__ uint32_t ld_hdr(const uint32_t *d, uint32_t blen, uint32_t c) {
     return c < blen && blen - c >= 7u ? lds32u(d, c + 3u) : 0u;
 }
-// z^(4k)(x) ^ w from 5-bit tables (k = 1..4: 4, 8, 12, 16 zero bytes; x: a
+// z^(4k)(x) ^ w from 5-bit tables (k = 1, 2: 4 or 8 zero bytes; x: a
 // chain's state XORed with its latest data dword):
 //   z^(4k)(x) = XOR_i F_k,i[(x >> 5i) & 31],  F_k,i[v] = z^(4k)(v << 5i), i = 0..6
 // (the last field 2 bits).  A 32-entry table fills the 32 banks a ds_read_b32
@@ -933,7 +937,7 @@ constexpr uint32_t kLDLongDw = 128;
 static_assert(kLDLongDw * 4u * kLCSlots >= 32768u, "a block holds fewer long records than slots");
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t nt[4 * kLDTabDwords];  // tables of z^4, z^8, z^12, z^16 (ld_map)
+    __shared__ uint32_t nt[2 * kLDTabDwords];  // tables of z^4, z^8 (ld_map)
     __shared__ uint32_t t0[256];
     __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
     __shared__ uint32_t run_b[kLDRuns];  // first event (of the pass) | type << 16 | kind << 24
@@ -951,7 +955,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     t0[t] = A.aux[t];
     if (t < 3) s_m[t] = kLCNone;
     ld_sync();
-    for (uint32_t w = t; w < 4u * kLDTabDwords; w += kLDThreads) {
+    for (uint32_t w = t; w < 2u * kLDTabDwords; w += kLDThreads) {
         // F_k,i[v] = z^(4k)(v << 5i) at 224 (k-1) + 32 i + v (i = 6: v < 4, the rest unused)
         const uint32_t k = w / kLDTabDwords + 1u, e = w % kLDTabDwords;
         const uint32_t i = e >> 5, v = e & 31u;
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         t0[e >> 24] = (e << 8) | t;
     }
     ld_sync();
-    const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords, *N12 = nt + 2 * kLDTabDwords, *N16 = nt + 3 * kLDTabDwords;
+    const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords;
     // the first dword of a record whose crc range starts q & 3 = h bytes into a
     // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
     // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
@@ -1070,22 +1074,23 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
                 x0 = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
             }
-            // four chains: the record's dwords end-aligned on groups of 4 (o zero
-            // dwords in front), chain c takes position c of every group and steps
-            // z^16; at the end chain c still owes z^(16 - 4c)
-            const uint32_t o = (4u - (nd & 3u)) & 3u, G = (nd + o) >> 2;
+            // two chains: the record's dwords end-aligned on pairs (o zero dwords in
+            // front), chain c takes position c of every pair and steps z^8; at the
+            // end chain 0 still owes z^4.  r4 ran four chains stepping z^16 and
+            // folded them with z^12 / z^8 / z^4 (21 lookups per record against 7):
+            // the crc phase is bound by the CU's LDS pipe and VALU issue together,
+            // not by latency, so the fold's lookups cost more than the ILP gained
+            // (r5l, same box: DBBench 1.274 -> 1.242 ms, random lengths 2.643 ->
+            // 2.602)
+            const uint32_t o = nd & 1u, G = (nd + o) >> 1;
             const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
-            uint32_t y[4];
-#pragma unroll
-            for (uint32_t c = 0; c < 4; c++) y[c] = c < o ? 0u : (c == o ? x0 : D[c]);
+            uint32_t y0 = o ? 0u : x0, y1 = o ? x0 : D[1];
             for (uint32_t g = 1; g < G; g++) {
-                uint32_t v[4];
-#pragma unroll
-                for (uint32_t c = 0; c < 4; c++) v[c] = D[4u * g + c];
-#pragma unroll
-                for (uint32_t c = 0; c < 4; c++) y[c] = ld_map(N16, y[c], v[c]);
+                const uint32_t v0 = D[2u * g], v1 = D[2u * g + 1u];
+                y0 = ld_map(N8, y0, v0);
+                y1 = ld_map(N8, y1, v1);
             }
-            const uint32_t sv = ld_map(N12, y[0]) ^ ld_map(N8, y[1]) ^ ld_map(N4, y[2]) ^ y[3];
+            const uint32_t sv = ld_map(N4, y0, y1);
             if (sv != want) atomicMin(&s_bad, h);
         };
         auto doff16 = [&](uint32_t r) { return (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu; };
@@ -1273,7 +1278,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
 
 // as many workgroups per CU as the LDS holds
 uint32_t lc_dense_grid(int cus) {
-    constexpr uint32_t lds = (8192 + 4) * 4 + 4 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + kDWMax * 2 + 64;
+    constexpr uint32_t lds = (8192 + 4) * 4 + 2 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + kDWMax * 2 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
 hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st) {
