@@ -716,8 +716,8 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 //          (J/db/LogReader.java:297-383, the reference's decisions in its order)
 //   crc    one thread per OK record, table lookups that never conflict (ld_map:
 //          5-bit tables, one copy each): the record's dwords end-aligned in
-//          groups of 4, four chains (position c of every group) stepping z^16,
-//          folded at the end with z^16 / z^12 / z^8 / z^4;
+//          pairs, two chains (position c of every pair) stepping z^8, folded
+//          at the end with one z^4;
 //          the record's first bytes are seeded with W0 (the 4 bytes before it
 //          that take state 0 to value()'s 0xffffffff, so the first dword needs
 //          no byte tables), its last dword is zero-padded and the stored crc
@@ -739,7 +739,10 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // at the first record that is not OK (lc_dense's walk decides it, as it decides
 // the rest of the block), and at a run of kDWRun equal records (lc_dense's trips
 // measure runs 257 records at a time: DBBench's blocks leave here after 8 hops).
-// Offsets are u16 (p < 32 KiB), eight per 16-B store.
+// Offsets are u16 (p < 32 KiB), eight per 16-B store.  The walk reads nearly
+// every line of its blocks at the HBM's random-line rate: a line prefetch 256 or
+// 512 B ahead of each lane's walk made it slower (r5p, random 0-200 B set 2.62 ->
+// 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2).
 __global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= A.dense_ctr[0]) return;
@@ -1057,7 +1060,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             }
             // the record's last dword is read whole: its 4 - tl bytes past the record
             // (the next header's) enter the chains' result s linearly, as themselves
-            // (the last dword is chain 3's last word, XORed in unshifted), so s is
+            // (the last dword is chain 1's last word, XORed in unshifted), so s is
             // compared with want ^ those bytes instead of masking the dword in the loop
             const uint32_t gmask = tl ? ~((1u << (8u * tl)) - 1u) : 0u;
             // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last dword
@@ -1081,7 +1084,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             // the crc phase is bound by the CU's LDS pipe and VALU issue together,
             // not by latency, so the fold's lookups cost more than the ILP gained
             // (r5l, same box: DBBench 1.274 -> 1.242 ms, random lengths 2.643 ->
-            // 2.602)
+            // 2.602).  Issuing both chains' 14 lookups together (the compiler
+            // waits for chain 0's before reusing its registers for chain 1's
+            // addresses) was no faster either (r5n: 1.264 vs 1.255 ms)
             const uint32_t o = nd & 1u, G = (nd + o) >> 1;
             const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
             uint32_t y0 = o ? 0u : x0, y1 = o ? x0 : D[1];
