@@ -57,9 +57,12 @@ __device__ __forceinline__ uint32_t step(const uint32_t *lds, const Lanes &g, ui
     return (v0 ^ v1) ^ (v2 ^ v3);
 }
 
-template <int MODE>  // 0: one record at a time; 1: the next record's loads issued before this one's steps
+// MODE 0: one record at a time; 1: the next record's loads issued before this one's steps.
+// wrap: records taken modulo `wrap` (a window that stays in L2: the load path alone)
+template <int MODE>
 __global__ __launch_bounds__(1024) void probe(const uint8_t *__restrict__ log, const uint32_t *__restrict__ img,
-                                              uint64_t nrec, uint32_t *__restrict__ out, int write_all) {
+                                              uint64_t nrec, uint32_t *__restrict__ out, int write_all,
+                                              uint64_t wrap = ~0ull) {
     __shared__ uint32_t lds[kLds];
     for (uint32_t i = threadIdx.x; i < kLds; i += blockDim.x) lds[i] = img[i];
     __syncthreads();
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(1024) void probe(const uint8_t *__restrict__ log, c
     uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
     auto ld = [&](uint64_t rr, v4u *w) {
-        const uint8_t *a = log + ((rr * kRec + kOff) & ~3ull);
+        const uint8_t *a = log + (((rr % wrap) * kRec + kOff) & ~3ull);
 #pragma unroll
         for (int j = 0; j < 9; j++) w[j] = *(const v4u_a4 *)(a + 16 * j);
     };
@@ -143,9 +146,9 @@ int main(int argc, char **argv) {
     for (int mode = 0; mode < 2; mode++) {
         CK(hipMemset(out, 0, nchk * 4));
         if (mode == 0)
-            hipLaunchKernelGGL(probe<0>, dim3(4), dim3(1024), 0, 0, log, dimg, nchk, out, 1);
+            hipLaunchKernelGGL(probe<0>, dim3(4), dim3(1024), 0, 0, log, dimg, nchk, out, 1, ~0ull);
         else
-            hipLaunchKernelGGL(probe<1>, dim3(4), dim3(1024), 0, 0, log, dimg, nchk, out, 1);
+            hipLaunchKernelGGL(probe<1>, dim3(4), dim3(1024), 0, 0, log, dimg, nchk, out, 1, ~0ull);
         CK(hipDeviceSynchronize());
         std::vector<uint32_t> got(nchk);
         CK(hipMemcpy(got.data(), out, nchk * 4, hipMemcpyDeviceToHost));
@@ -167,17 +170,18 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int mode = 0; mode < 2; mode++)
-        for (int wpc : {1, 2, 4}) {  // workgroups of 1024 threads per CU (1: the LDS of one)
-            if (wpc > 1) continue;    // 128 KiB of LDS: one workgroup per CU
+    for (int mode = 0; mode < 4; mode++)
+        for (int wpc : {1}) {  // workgroups of 1024 threads per CU (128 KiB of LDS: one per CU)
             const int grid = cus * wpc;
+            // modes 2 / 3: as 1, records modulo a 2 MiB / 32 MiB window (L2 / Infinity Cache resident)
+            const uint64_t wrap = mode == 2 ? (2u << 20) / kRec : mode == 3 ? (32u << 20) / kRec : ~0ull;
             float best = 1e9f, sum = 0;
             for (int rep = 0; rep < 8; rep++) {
                 CK(hipEventRecord(e0));
                 if (mode == 0)
-                    hipLaunchKernelGGL(probe<0>, dim3(grid), dim3(1024), 0, 0, log, dimg, nrec, out, 0);
+                    hipLaunchKernelGGL(probe<0>, dim3(grid), dim3(1024), 0, 0, log, dimg, nrec, out, 0, ~0ull);
                 else
-                    hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(1024), 0, 0, log, dimg, nrec, out, 0);
+                    hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(1024), 0, 0, log, dimg, nrec, out, 0, wrap);
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 float ms;
