@@ -13,6 +13,11 @@
  *   - "_dev" functions take device pointers (HBM) and a hipStream_t (void*;
  *     NULL = the HIP null stream) and are asynchronous unless noted;
  *     the other batch functions take host memory and block until done;
+ *   - the "_dev" compute functions (not jl_fill_random_dev / jl_read_stream_dev)
+ *     refuse a stream that is being captured into a HIP graph with
+ *     JL_ERR_INVALID, before enqueueing anything: scratch sizing and the
+ *     ordering of a thread's calls are host-side, per call, and a replay would
+ *     bypass them;
  *   - thread-safe: every calling thread gets its own streams, pinned staging
  *     and device scratch (created on its first call, freed when it exits), so
  *     concurrent callers do not serialise; jl_init / jl_shutdown must not race

@@ -517,6 +517,25 @@ int ensure_chunk_bufs(Workspace &w, const std::vector<Chunk> &ch, size_t out_byt
 // entry points order with the caller's default-stream work.
 hipStream_t pick(void *stream) { return (hipStream_t)stream; }
 
+// The device entry points refuse a stream that is being captured into a HIP
+// graph: their per-thread scratch and the bookkeeping around it (the pending
+// asynchronous call's event, scratch sizing, the host read-backs of the
+// synchronous forms, stream-ordered scratch allocations) is done on the host
+// at call time, so a replayed graph would run against state the host no longer
+// tracks.  r5 replayed a captured jl_log_verify_dev_async and it faulted.
+int no_capture(void *stream, const char *who) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(pick(stream), &cs);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(JL_ERR_INVALID, std::string(who) + ": stream capture (HIP graphs) is not supported (" +
+                                        hipGetErrorString(e) + ")");
+    }
+    if (cs != hipStreamCaptureStatusNone)
+        return fail(JL_ERR_INVALID, std::string(who) + ": stream capture (HIP graphs) is not supported");
+    return JL_OK;
+}
+
 int grid_for(uint64_t blocks) {
     // one 1024-thread workgroup (16 waves) per CU; fewer when there is little work
     uint64_t wg = (blocks + 15) / 16;
@@ -866,6 +885,7 @@ int jl_shutdown(void) {
 int jl_crc32c_fixed_dev(const void *d_data, uint64_t block_bytes, uint64_t n_blocks, uint32_t flags,
                         uint32_t *d_out, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_crc32c_fixed_dev")) return r;
     if (n_blocks == 0) return JL_OK;
     if (!d_data || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: null pointer");
     if (block_bytes > 0xffffffffull) return fail(JL_ERR_INVALID, "jl_crc32c_fixed_dev: block_bytes >= 4 GiB");
@@ -919,6 +939,7 @@ int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t 
                         const uint32_t *d_init, const uint8_t *d_suffix, uint64_t n, uint32_t flags, uint32_t *d_out,
                         void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_crc32c_batch_dev")) return r;
     if (n == 0) return JL_OK;
     if (!d_base || !d_off || !d_len || !d_out) return fail(JL_ERR_INVALID, "jl_crc32c_batch_dev: null pointer");
     jlk::KParams P = base_params(d_base, n, jlk::MODE_CRC);
@@ -983,6 +1004,7 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
 int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint32_t *d_size, const uint8_t *d_type,
                           uint64_t n, uint8_t *d_trailer, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_table_trailers_dev")) return r;
     if (n == 0) return JL_OK;
     if (!d_file || !d_off || !d_size || !d_trailer) return fail(JL_ERR_INVALID, "jl_table_trailers_dev: null pointer");
     jlk::KParams P = base_params(d_file, n, jlk::MODE_TRAILER);
@@ -996,6 +1018,7 @@ int jl_table_trailers_dev(const void *d_file, const uint64_t *d_off, const uint3
 int jl_table_verify_dev(const void *d_file, uint64_t file_bytes, const uint64_t *d_off, const uint32_t *d_size,
                         uint64_t n, uint8_t *d_status, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_table_verify_dev")) return r;
     if (n == 0) return JL_OK;
     if (!d_file || !d_off || !d_size || !d_status) return fail(JL_ERR_INVALID, "jl_table_verify_dev: null pointer");
     jlk::KParams P = base_params(d_file, n, jlk::MODE_TABLE_VERIFY);
@@ -1146,6 +1169,7 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
 int jl_log_headers_dev(const void *d_base, const uint64_t *d_off, const uint32_t *d_len, const uint8_t *d_type,
                        uint64_t n, uint8_t *d_header, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_log_headers_dev")) return r;
     if (n == 0) return JL_OK;
     if (!d_base || !d_off || !d_len || !d_type || !d_header)
         return fail(JL_ERR_INVALID, "jl_log_headers_dev: null pointer");
@@ -1161,6 +1185,7 @@ int jl_log_emit_dev(const void *d_src, const uint64_t *d_frag_hdr_off, const uin
                     const uint32_t *d_frag_len, const uint8_t *d_frag_type, uint64_t n_frags, uint64_t log_bytes,
                     uint8_t *d_log, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_log_emit_dev")) return r;
     if (n_frags == 0 && log_bytes == 0) return JL_OK;
     if (!d_log || (n_frags && (!d_src || !d_frag_hdr_off || !d_frag_src_off || !d_frag_len || !d_frag_type)))
         return fail(JL_ERR_INVALID, "jl_log_emit_dev: null pointer");
@@ -1411,6 +1436,7 @@ static int ws_after(Workspace &w, hipStream_t st, bool async, int rc) {
 int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                       uint64_t *n_events, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_log_verify_dev")) return r;
     if (!n_events || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev: null pointer");
     if (checksum < 0 || checksum > JL_LOG_CHECKSUM_FUSED) return fail(JL_ERR_INVALID, "jl_log_verify_dev: bad checksum mode");
     Workspace *w = nullptr;
@@ -1423,6 +1449,7 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
 int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum, jl_log_event *d_events, uint64_t cap,
                             uint64_t *d_result, void *stream) {
     if (int r = ensure_ready()) return r;
+    if (int r = no_capture(stream, "jl_log_verify_dev_async")) return r;
     if (!d_result || (log_bytes && !d_log)) return fail(JL_ERR_INVALID, "jl_log_verify_dev_async: null pointer");
     if (checksum < 0 || checksum > JL_LOG_CHECKSUM_TWO_PASS)
         return fail(JL_ERR_INVALID, "jl_log_verify_dev_async: bad checksum mode");

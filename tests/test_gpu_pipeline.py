@@ -223,6 +223,37 @@ def test_async_then_empty_sync_call_then_device_call(gpu, jl, oracle, log_image)
                           _live(oracle.log_events(log_image[CH: CH + (80 << 20)])))
 
 
+def test_stream_capture_refused(gpu, jl, oracle, log_image):
+    """A device entry point called on a stream being captured into a HIP graph
+    returns JL_ERR_INVALID before it enqueues anything (the per-call host
+    bookkeeping cannot be replayed; jlcrc.h conventions); the thread's engine
+    state is unharmed: the next uncaptured call equals the oracle."""
+    import torch
+
+    a = torch.from_numpy(log_image[: 8 << 20].copy()).to(gpu)
+    ev = torch.zeros((a.numel() // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
+    res = torch.zeros(3, dtype=torch.int64, device=gpu)
+    off = torch.arange(0, 64, dtype=torch.int64, device=gpu) * 4096
+    ln = torch.full((64,), 4096, dtype=torch.int32, device=gpu)
+    out = torch.zeros(64, dtype=torch.int32, device=gpu)
+    s = torch.cuda.Stream()
+    errs = []
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        for fn in (lambda: jl.log_verify_dev_async(a, events=ev, result=res, stream=s),
+                   lambda: jl.crc32c_batch_dev(a, off, ln, out=out, stream=s)):
+            try:
+                fn()
+            except jl.JLError as e:
+                errs.append(str(e))
+    assert len(errs) == 2 and all("stream capture" in e for e in errs), errs
+    ev2, n2 = jl.log_verify_dev(a)
+    torch.cuda.synchronize()
+    assert np.array_equal(_live(ev2[: n2 * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)),
+                          _live(oracle.log_events(log_image[: 8 << 20])))
+
+
 @pytest.mark.parametrize("mode", ["staged", "pinned"])
 def test_dense_log_host(gpu, jl, oracle, engine_options, mode):
     """~150 MiB DBBench-default log (131-B payloads: every 32 KiB block dense) with
