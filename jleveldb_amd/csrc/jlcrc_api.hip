@@ -122,6 +122,10 @@ struct Workspace {
     // a valid stream, HIP's null stream: `async_pending` says whether there is one);
     // async_done is recorded on that stream after its launches
     bool async_pending = false;
+    // the chunked log verification's four work counters (ws_lc's first 256 B) are
+    // zeroed by the last kernel of each verification for the next one; a call that
+    // stopped between its launches (or a new ws_lc) leaves them to a memset
+    bool lc_dirty = true;
     hipStream_t async_st = nullptr;
     hipEvent_t async_done = nullptr;
     Slot slot[2];
@@ -1278,12 +1282,14 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     const uint64_t nb = (log_bytes + 32767) / 32768, ng = (nb + jlk::kLCGroup - 1) / jlk::kLCGroup;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t hn = jlk::kLCCounters * ng + 1;
-    const size_t o_cnt = 0, o_start = al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
+    const size_t o_cnt = 256, o_start = o_cnt + al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
                  o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
                  o_di = o_nl + al(nb * 4), o_dw = o_di + al(nb * 4), o_end = o_dw + al(nb * jlk::kDWMax * 2);
+    const size_t lc_cap = c.ws_lc.cap;
     JL_HIP(c.ws_lc.ensure(o_end));
+    if (c.ws_lc.cap != lc_cap) c.lc_dirty = true;  // a new buffer: its counters are not zero
     JL_HIP(c.ws_slot.ensure(nb * jlk::kLCSlots * 8));
     // The dense blocks' runs of events (lc_dense): no more runs than events, and
     // at most the caller's capacity of events (more fail the call anyway), plus one
@@ -1321,7 +1327,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.dense_off = (uint64_t *)(ws + o_do);
     A.cap_flag = (uint32_t *)(ws + o_flag);
     A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
-    A.dense_ctr = (uint32_t *)(ws + o_flag + 16);
+    A.dense_ctr = (uint32_t *)ws;  // at a fixed place: the previous verification zeroed it
     A.dense_list = (uint32_t *)(ws + o_dl);
     A.nlong = (uint32_t *)(ws + o_nl);
     A.dw_info = (uint32_t *)(ws + o_di);
@@ -1338,7 +1344,10 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
     // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
-    JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
+    // (lc_finish zeroes them again at the end; r5 dropped the memset here: a
+    // 4.4 us fill dispatch plus a ~6 us gap before it in every verification)
+    if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
+    c.lc_dirty = true;  // until the last launch of this verification is enqueued
     JL_HIP(jlk::launch_lc_walk(A, st));
     // the dense blocks' headers (lc_dwalk, one lane per block), then their crcs
     // (lc_dense).  r5 measured lc_dwalk of half the list on a second stream beside
@@ -1369,7 +1378,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         G.P.out32 = A.first_bad;
         G.desc = A.desc;
         G.n_rounds = A.rstart + jlk::kLCBins;
-        G.deal = A.dense_ctr + 2;  // zeroed with dense_ctr before lc_walk
+        G.deal = A.dense_ctr + 2;  // zero when the verification starts (lc_finish of the one before)
         G.seed0 = jlmath::slice4_inv(0xffffffffu);
         G.parts = A.parts;
         G.study = (uint32_t)opt().gv4_variant;  // 0 unless a study build set JL_OPT_GV4_VARIANT
@@ -1377,6 +1386,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));
     }
+    c.lc_dirty = false;  // lc_finish (lc_apply, or lc_build without checksums) zeroes the counters
     if (d_result) return JL_OK;  // asynchronous: the caller reads d_result in stream order
     // events, dense blocks, capacity flag (lc_finish, written to c.h_res by the
     // last kernel): wait by polling the stream (a blocking synchronise sleeps,

@@ -166,7 +166,7 @@ struct LCArgs {
     uint32_t *first_bad;   // n_blocks: header offset of the block's first failing record
     uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range
     uint32_t *dense_list;  // n_blocks: the dense blocks (lc_walk appends, lc_dense takes them in chunks)
-    uint32_t *dense_ctr;   // [0] dense blocks listed, [1] list entries taken, [2] gv4 deal, [3] lc_scan ids (zeroed before lc_walk)
+    uint32_t *dense_ctr;   // [0] dense blocks listed, [1] list entries taken, [2] gv4 deal, [3] lc_scan ids (zero at the start; lc_finish re-zeroes them)
     uint32_t *cap_flag;    // set when a capacity was exceeded
     uint64_t *result;      // [0] events, [1] dense blocks, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8

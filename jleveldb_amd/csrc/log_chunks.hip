@@ -306,8 +306,8 @@ __device__ __forceinline__ uint32_t ls_block_excl(uint32_t v, uint32_t *wsum, ui
 }
 constexpr uint32_t kLSPer = kLSTile / 256u;  // values per thread
 static_assert(kLSTile % 256u == 0u, "kLSTile: a multiple of the workgroup");
-// Work ids come from a counter in dispatch order (dense_ctr[3], zeroed before
-// lc_walk), not from blockIdx.x: tile k's look-back spins on tiles k - 1 ..., so
+// Work ids come from a counter in dispatch order (dense_ctr[3], zero when
+// lc_walk starts), not from blockIdx.x: tile k's look-back spins on tiles k - 1 ..., so
 // it must not run before they have started, which a blockIdx order would only
 // assume of the hardware's dispatch (rocPRIM takes its tile ids the same way).
 __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
@@ -581,11 +581,15 @@ __device__ __forceinline__ void lc_expand_runs(const LCArgs &A, uint64_t b, uint
     }
 }
 
+// The last kernel of a verification (block 0, thread 0): the result words, and
+// the work counters zeroed for the next verification of this workspace (no
+// kernel of this one reads them after lc_build / gv4).
 __device__ __forceinline__ void lc_finish(const LCArgs &A) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         A.result[0] = A.start[A.n_blocks];
         A.result[1] = A.rowtot[kLCOver];
         A.result[2] = *A.cap_flag;
+        lc_st16(A.dense_ctr, lc_v4{0u, 0u, 0u, 0u});
     }
 }
 
