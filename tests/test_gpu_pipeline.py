@@ -271,3 +271,43 @@ def test_dense_log_host(gpu, jl, oracle, engine_options, mode):
     g, w = _live(jl.log_verify(buf)), _live(oracle.log_events(log))
     assert g.shape == w.shape and np.array_equal(g, w)
     assert int((w[3] == jl.LOG_BAD_CRC).sum()) + int((w[3] == jl.LOG_BAD_LENGTH).sum()) >= 3
+
+
+def test_work_counters_between_verifications(gpu, jl, oracle, log_image):
+    """The chunked verification's work counters (dense-block list, lc_dense's and
+    gv4's dealing, lc_scan's ids) are zeroed by each verification's last kernel
+    for the next one (a memset only for a new workspace).  A sequence on one
+    thread that grows the workspace, shrinks it, alternates dense and sparse
+    logs, walk-only and checksummed calls, and async and sync forms must give
+    the oracle's events every time."""
+    import torch
+
+    lens = wl.c5_lengths("dbbench_131", target=24 << 20, seed=SEED + 1)
+    plan = jl.log_layout(wl.packed_offsets(lens), lens)
+    src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(src, SEED + 21)
+    dense = jl.log_emit_dev(src, plan)
+    dense[4_000_000] ^= 0x20
+    dense_h = dense.cpu().numpy()
+    sparse_h = log_image[: 40 << 20]
+    sparse = torch.from_numpy(sparse_h.copy()).to(gpu)
+    small_h = log_image[: 3 << 20]
+    small = torch.from_numpy(small_h.copy()).to(gpu)
+    want = {}
+    for name, h in (("dense", dense_h), ("sparse", sparse_h), ("small", small_h)):
+        for cs in (0, 1):
+            want[name, cs] = _live(oracle.log_events(h, checksum=bool(cs)))
+    logs = {"dense": dense, "sparse": sparse, "small": small}
+    seq = [("small", 1, False), ("dense", 1, False), ("dense", 1, True), ("sparse", 1, False), ("small", 0, False),
+           ("dense", 0, True), ("dense", 1, False), ("sparse", 1, True), ("small", 1, True), ("dense", 1, True)]
+    for name, cs, use_async in seq:
+        t = logs[name]
+        if use_async:
+            ev = torch.zeros((t.numel() // 7 + 2) * 16, dtype=torch.uint8, device=gpu)
+            _, res = jl.log_verify_dev_async(t, bool(cs), events=ev)
+            torch.cuda.synchronize()
+            n = int(res.cpu()[0])
+        else:
+            ev, n = jl.log_verify_dev(t, bool(cs))
+        got = _live(ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE))
+        assert got.shape == want[name, cs].shape and np.array_equal(got, want[name, cs]), (name, cs, use_async)
