@@ -268,10 +268,16 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     // store a block's consecutive slots (a run of kLCLdsSlots x 8 B per block; one
     // thread per block writing its own slots touched 64 lines per store, 33 us of
     // the C5 walk).  Slots past a block's count are never read.
+    // Only the slots lc_build reads: a dense block's (lc_dense re-walks it) and the
+    // slots past a block's count are skipped (r5: the DBBench set's walk wrote
+    // 36 MB of abandoned slots).
+    __shared__ uint32_t s_used[256];
+    s_used[threadIdx.x] = listed ? 0u : cnt;
+    __syncthreads();
     const uint64_t b0 = (uint64_t)wg * 256u;
     for (uint32_t e = threadIdx.x; e < 256u * kLCLdsSlots; e += 256u) {
         const uint32_t t = e / kLCLdsSlots, j = e - t * kLCLdsSlots;
-        if (b0 + t < A.n_blocks) A.slots[(b0 + t) * kLCSlots + j] = ls[t][j];
+        if (b0 + t < A.n_blocks && j < s_used[t]) A.slots[(b0 + t) * kLCSlots + j] = ls[t][j];
     }
     const uint64_t g0 = (uint64_t)wg * 4u;
     for (uint32_t i = threadIdx.x; i < 4 * kLCCounters; i += 256u) {
