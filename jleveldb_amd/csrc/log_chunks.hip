@@ -606,7 +606,10 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         ctr[i] = A.checksum ? A.hscan[i * nw + blockIdx.x] : 0u;
     for (uint32_t i = threadIdx.x; i <= kLCBins && A.checksum; i += blockDim.x) rs[i] = A.rstart[i];
     __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    // the wave index as a uniform value: the blocks' counts, starts and dense
+    // offsets then load with scalar loads into SGPRs (118 -> 57 VGPRs, 2 -> 3
+    // workgroups per CU)
+    const uint32_t lane = threadIdx.x & 63u, wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // the wave's blocks wv, wv + 16, ... of the group: all their loads first
     constexpr uint32_t kPer = kLCGroup / kLCBuildWaves;
     uint32_t cnt[kPer], nl[kPer];
