@@ -112,7 +112,11 @@ const char *jl_version(void);
  *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
  *                            default 16 MiB (the driver's crossover; one ~4 MiB
  *                            WAL stays on the host)
- * Study builds only (make STUDY=1): JL_OPT_GV4_VARIANT (crc_gv4_kernel bound-study variants). */
+ *   JL_OPT_FAILPOINT         tests only: bit 0 perturbs the dense blocks' header
+ *                            offsets between lc_dwalk and lc_dense (a different
+ *                            inconsistency per block); results must not change
+ *                            (lc_dense re-walks such a block itself).  Default 0
+ */
 #define JL_OPT_GENERAL_PATH 1
 #define JL_OPT_STREAM_DEPTH 2
 #define JL_OPT_STREAM_PARTITION 3
@@ -122,7 +126,7 @@ const char *jl_version(void);
 #define JL_OPT_HOST_THRESHOLD 7
 #define JL_OPT_LOG_HOST_THRESHOLD 8
 #define JL_OPT_STAGE_PIECE 9
-#define JL_OPT_GV4_VARIANT 101
+#define JL_OPT_FAILPOINT 10
 #define JL_PATH_AUTO 0
 #define JL_PATH_STREAM 1
 #define JL_PATH_GV4 2

@@ -212,7 +212,7 @@ def shutdown() -> None:
 OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 3, 4
 OPT_HOST_REGISTER, OPT_STAGE_THREADS, OPT_HOST_THRESHOLD, OPT_LOG_HOST_THRESHOLD = 5, 6, 7, 8
 OPT_STAGE_PIECE = 9
-OPT_GV4_VARIANT = 101  # study builds only
+OPT_FAILPOINT = 10  # tests only
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
 
 
@@ -459,7 +459,11 @@ def log_verify(log, checksum: bool = True, out=None) -> np.ndarray:
         cap = size // 7 + 2
         ev = np.zeros(cap, dtype=LOG_EVENT_DTYPE)
     else:
-        assert out.dtype == LOG_EVENT_DTYPE and out.flags.c_contiguous
+        # checked here, not by assert (python -O): the engine writes through out's pointer
+        if not isinstance(out, np.ndarray) or out.dtype != LOG_EVENT_DTYPE:
+            raise TypeError("log_verify: out must be a numpy array of LOG_EVENT_DTYPE")
+        if not out.flags.c_contiguous or not out.flags.writeable:
+            raise ValueError("log_verify: out must be C-contiguous and writeable")
         ev, cap = out, out.size
     n = ctypes.c_uint64(0)
     _check(lib().jl_log_verify(ptr if size else None, size, int(checksum), ev.ctypes.data, cap,

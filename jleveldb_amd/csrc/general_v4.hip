@@ -42,9 +42,6 @@
 
 #include "engine_device.hpp"
 
-#ifndef JL_STUDY
-#define JL_STUDY 0
-#endif
 #ifndef JL_MODE
 #error "compile with -DJL_MODE=<jlk::MODE_*>"
 #endif
@@ -142,19 +139,9 @@ constexpr uint32_t kLCMB = 16384, kLCSelB = 30720;
 #define JL_RING_SLACK 2
 #endif
 
-// Study builds (tools/build_study.sh ... -DJL_GV4_WAVETIME=1): every wave's start
-// and end time (s_memrealtime, 100 MHz, one clock for the whole chip), read with
-// jl_study_gv4_wavetime_m<mode> (tools/gv4_wavetime.py): how long the last waves
-// run after the others have finished (the grid's tail).
-#ifndef JL_GV4_WAVETIME
-#define JL_GV4_WAVETIME 0
-#endif
-#if JL_GV4_WAVETIME
-#define JL_WT_CAT2(a, b) a##b
-#define JL_WT_CAT(a, b) JL_WT_CAT2(a, b)
-#define JL_WT_ARR JL_WT_CAT(g_gv4_wt_m, JL_MODE)
-__device__ unsigned long long JL_WT_ARR[2 * 16384];
-#endif
+// (The per-wave start / end timing study of r4, JL_GV4_WAVETIME with
+// tools/gv4_wavetime.py, and the bound-study variants of this kernel live on the
+// branch study-r5-gv4-switches.)
 
 template <int MODE>
 struct GV4 {
@@ -298,7 +285,7 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 // at the same rate — issue goes to the oldest first — so on C3 the waves of
 // slots 0-3 finished at ~1.0 ms, slots 4-7 at ~1.3, 8-11 at ~1.7 and 12-15 at
 // ~1.9 ms, and the kernel ran its last ~0.8 ms with ever fewer loads in flight
-// (tools/gv4_wavetime.py, profiles/r4i_gv4_wavetime.json); dealt dynamically but
+// (tools/gv4_wavetime.py on the branch study-r5-gv4-switches, profiles/r4i_gv4_wavetime.json); dealt dynamically but
 // still ascending, C3's heaviest rounds (8 blocks of 64 KiB, ~0.3 ms for one
 // wave) came last and left a 0.4 ms tail (r4j).  The taken rounds go through a
 // 16-entry queue per wave in LDS: the prefetch cursor takes round i (and i + 1,
@@ -323,29 +310,18 @@ __device__ __forceinline__ uint32_t n_entries(const GV4Args &A, uint32_t K) {
 // 1.2-3.3 ms; batches from the first round on put C3's heaviest rounds on a few
 // workgroups (64 per batch: 2.0 -> 2.43 ms), hence the static head.  Without a
 // counter (implicit rounds), the stride above.
-#ifndef JL_GV4_DEAL
-#define JL_GV4_DEAL 1
-#endif
-#ifndef JL_GV4_DEAL_BATCH
-#define JL_GV4_DEAL_BATCH 32
-#endif
 // batch size min(kGvDealBatch, R / (64 G)): every workgroup still takes >= ~48
 // batches (the tail's granularity), and a call of fewer than 64 G rounds keeps
-// the stride (its batches would leave most CUs idle)
-constexpr uint32_t kGvDealBatch = JL_GV4_DEAL_BATCH;
-#ifndef JL_GV4_STATIC_DIV
-#define JL_GV4_STATIC_DIV 4
-#endif
-constexpr uint32_t kGvStaticDiv = JL_GV4_STATIC_DIV;
+// the stride (its batches would leave most CUs idle).  The static head is the
+// heaviest 1/kGvStaticDiv of the rounds (r4w: 1/2 and 1/8 within +-0.5 %).
+constexpr uint32_t kGvDealBatch = 32;
+constexpr uint32_t kGvStaticDiv = 4;
 constexpr uint32_t kGvTagBits = 26, kGvTagMask = (1u << kGvTagBits) - 1u;  // reads <= kGvDealBatch < 64
 static_assert(kGvDealBatch < 64u, "a slot's read count takes 6 bits");
 constexpr uint32_t kGvNoRound = 0xffffffffu;  // >= any round count (< 2^31)
 
 // Prefetch cursor: walks the wave's rounds (seq(i), from the workgroup's counter) entry by entry.
-// L2W (study variant 7): every round's bytes are read from a 1 MiB window at the
-// start of the arena instead (the same round table and addressing pattern, the
-// data L2-resident: the CRC math without the HBM stream).
-template <int MODE, bool DBG, bool L2W = false>
+template <int MODE>
 struct GPF {
     uint32_t r, R, G, bx;  // rounds (< 2^31); the workgroup's rounds are j G + bx
     uint32_t i;            // r = seq(i)
@@ -370,7 +346,7 @@ struct GPF {
         uint32_t j = 0;
         if (lane0) j = atomicAdd(ctr, 1u);
         j = uni(j);
-        if (JL_GV4_DEAL && deal && j >= J0) {  // batches of rounds from the device counter
+        if (deal && j >= J0) {  // batches of rounds from the device counter
             const uint32_t k = j - J0, X0 = J0 * G;
             const uint32_t b = k / DB, o = k - b * DB;
             // slot s = {base, tag}: tag = (batch + 1) mod 2^kGvTagBits | rounds of that
@@ -444,11 +420,7 @@ struct GPF {
         const uint32_t rn = seq(i + 1u);
         vec_next = A.desc && E > (uint32_t)JL_GV4_RING && (k == 0u || Eprev >= (uint32_t)JL_GV4_RING) && rn < R;
         if (vec_next) desc_issue(A, rn, q, (k + 1u) & 1u);
-        uint64_t p = v.p;
-        if constexpr (L2W) {
-            const uint64_t b0 = (uint64_t)(uintptr_t)A.P.base & ~(uint64_t)127;
-            p = b0 + ((p - b0) & ((1u << 20) - 1u));
-        }
+        const uint64_t p = v.p;
         const uint64_t n = (uint64_t)K * 128u - (p & 127u) - v.d;
         const uint64_t pa = p & ~(uint64_t)15;
         addr = (p & ~(uint64_t)127) + 16u * l;
@@ -493,23 +465,6 @@ struct GPF {
     // would give the slot's new value a phi at the join, and the register
     // allocator may resolve that phi with a copy of the still-in-flight register.
     __device__ __forceinline__ uint64_t next(const GV4Args &A, uint32_t lane) {
-        const uint64_t a = next_raw(A, lane);
-        if (DBG && A.P.dbg) {  // debugging (JL_GV4_DEBUG): log and neutralise loads outside the valid range
-            const uint64_t zp = dummy - 16u * lane;
-            if (!((a >= A.P.dbg_lo && a + 16 <= A.P.dbg_hi) || (a >= zp && a + 16 <= zp + 4096))) {
-                const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
-                if (slot < 256) {
-                    A.P.dbg[1 + 4 * slot] = r;
-                    A.P.dbg[2 + 4 * slot] = e;
-                    A.P.dbg[3 + 4 * slot] = lane;
-                    A.P.dbg[4 + 4 * slot] = a;
-                }
-                return dummy;
-            }
-        }
-        return a;
-    }
-    __device__ __forceinline__ uint64_t next_raw(const GV4Args &A, uint32_t lane) {
         if (r >= R) return dummy;  // past the wave's last round: keep the ring count exact
         const uint32_t e0 = GV4<MODE>::side(A) ? 1u : 0u;
         uint64_t a;
@@ -531,19 +486,14 @@ struct GPF {
     }
 };
 
-// VAR: 0 = default (nt ring loads), 1 = strict (vmcnt(0) before every ring use:
-// debugging), 2 = ring loads without nt (cache-policy study), 3 = whole 8-entry
-// fast turns (study), 4 = address checks (JL_GV4_DEBUG), 5 = no fast path (study),
-// 6 = no step math (the loads, ring and round bookkeeping with a plain XOR per
-// step: the memory side alone; results wrong), 7 = the data of every round from
-// an L2-resident 1 MiB window (the math side alone; results wrong), 8 = no
-// epilogue math, 9 = no pad / seed handling in the first and last steps (8, 9:
-// per-round cost studies; results wrong)
-template <int MODE, int VAR = 0>
+// (r3-r5 measured bound-study variants of this kernel: strict waits, loads
+// without nt, whole 8-entry fast turns, address checks, no fast path, no step
+// math, L2-resident data, no epilogue math, no pad / seed handling — DESIGN.md
+// §4.2; they live on the branch study-r5-gv4-switches.)
+template <int MODE>
 __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__restrict__ img, GV4Args A,
                                                        const uint8_t *__restrict__ zero) {
     constexpr int P_ = JL_GV4_RING;
-    constexpr bool DBG = VAR == 4;  // JL_GV4_DEBUG builds the address checks in
     __shared__ uint32_t lds[kImageBytes / 4];
     load_image(lds, img);
     const uint32_t *ldsG = lds + kGOff / 4u;  // the G tables (rotated image)
@@ -556,15 +506,11 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     // blockIdx-major ids they all landed on the first ~60 CUs)
     const uint32_t G = gridDim.x, b = blockIdx.x;
     const uint32_t bx = (G & 7u) ? b : (b & 7u) * (G >> 3) + (b >> 3);
-#if JL_GV4_WAVETIME
-    const uint32_t w = uni((threadIdx.x >> 6) * G + bx);
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     const uint32_t R = A.desc ? *A.n_rounds : (uint32_t)((A.P.n + 7u) / 8u);  // rounds < 2^31
     (void)waves;
     // the prefetch cursor takes the wave's first round with K > 0 (round dealing
     // above); the compute cursor starts on the same one
-    GPF<MODE, DBG, VAR == 7> pf;
+    GPF<MODE> pf;
     pf.init(A, lds, G, bx, R, lane, (uint64_t)(uintptr_t)zero + 16u * lane);
     if (pf.r >= R) return;  // the workgroup's rounds are all taken: no ring started
     uint32_t ci = pf.i, cr = pf.r;
@@ -582,12 +528,8 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     // load (which declares the slot clobbered), the wait, and the reads (the
     // chains' final XOR takes the data word straight from the slot register).
 #define JL_GLD(RQ, ADDR, OFF, R0, R1, R2, R3)                                                                  \
-    if constexpr (VAR == 2)                                                                                    \
-        asm volatile("global_load_dwordx4 " RQ ", %0, off offset:%1" ::"v"(ADDR), "n"(OFF)                     \
-                     : "memory", R0, R1, R2, R3);                                                              \
-    else                                                                                                       \
-        asm volatile("global_load_dwordx4 " RQ ", %0, off offset:%1 nt" ::"v"(ADDR), "n"(OFF)                  \
-                     : "memory", R0, R1, R2, R3);
+    asm volatile("global_load_dwordx4 " RQ ", %0, off offset:%1 nt" ::"v"(ADDR), "n"(OFF)                      \
+                 : "memory", R0, R1, R2, R3);
 #define JL_LOAD(RQ, R0, R1, R2, R3)                                                                            \
     {                                                                                                          \
         const uint64_t a_ = pf.next(A, lane);                                                                  \
@@ -605,13 +547,6 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     auto rare = [&](v4u wv) {
         if (ce < e0) {
             side_c = wv;
-            return;
-        }
-        if constexpr (VAR == 9) {  // study: first / last steps as plain steps (no pads, no seed)
-            x0 = gstep_x3(ldsG, ce == e0 ? 0u : x0, gl, wv.x);
-            x1 = gstep_x3(ldsG, ce == e0 ? 0u : x1, gl, wv.y);
-            x2 = gstep_x3(ldsG, ce == e0 ? 0u : x2, gl, wv.z);
-            x3 = gstep_x3(ldsG, ce == e0 ? 0u : x3, gl, wv.w);
             return;
         }
         const uint32_t f = GV4<MODE>::LOGC ? cv.f : (uint32_t)(cv.p & 127u);
@@ -669,9 +604,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
         const uint32_t d = cv.d;
         const uint32_t col = ((l + (d >> 4)) & 15u) | ((q & 1u) << 4);
         uint32_t st;
-        if constexpr (VAR == 8) {  // study: no epilogue math (the chains XOR-folded as they are)
-            st = group_xor<8>(xor3(x0, x1, x2) ^ x3 ^ col);
-        } else if constexpr (GV4<MODE>::LOGC) {
+        if constexpr (GV4<MODE>::LOGC) {
             // chain j: its pending gap step, then z^-(4 (j + c) + e), in one table
             // (uniform d mod 16; crc_math.hpp build_lds_image_logchunk)
             const uint32_t sm = kLCMB + 512u * (d & 15u);
@@ -702,15 +635,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
             st = (st >> 8) ^ lds_at(lds, kT0B + (((st ^ sfx) & 0xffu) << 2));
         }
         const uint32_t crc = ~st, m = mask_crc(crc);
-        if (DBG && A.P.dbg && l == 0u && cv.idx < kGPart && cv.idx >= A.P.n) {
-            const unsigned long long slot = atomicAdd(A.P.dbg, 1ull);
-            if (slot < 256) {
-                A.P.dbg[1 + 4 * slot] = cr;
-                A.P.dbg[2 + 4 * slot] = 0xffff;
-                A.P.dbg[3 + 4 * slot] = lane;
-                A.P.dbg[4 + 4 * slot] = cv.idx;
-            }
-        } else if (l == 0u && cv.idx != kGNull) {
+        if (l == 0u && cv.idx != kGNull) {
             if constexpr (GV4<MODE>::LOGC) {
                 if (cv.idx >= kGPart) {
                     A.parts[cv.idx - kGPart] = raw;
@@ -772,11 +697,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
                             lds_at(ldsG, JL_GADDR(gl.l1, x, 2u)));                                         \
     const uint32_t A3 = lds_at(ldsG, JL_GADDR(gl.l0, x, 3u));
 #define JL_XS4(R0, R1, R2, R3)                                                                             \
-    if constexpr (VAR == 6) {                                                                              \
-        asm volatile("v_xor_b32 %0, %0, " R0 "\n\tv_xor_b32 %1, %1, " R1 "\n\tv_xor_b32 %2, %2, " R2        \
-                     "\n\tv_xor_b32 %3, %3, " R3                                                            \
-                     : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));                                             \
-    } else {                                                                                               \
+    {                                                                                                      \
         JL_LK(x0, t0_, u0_) JL_LK(x1, t1_, u1_) JL_LK(x2, t2_, u2_) JL_LK(x3, t3_, u3_)                    \
         asm volatile("v_bitop3_b32 %0, %4, %5, " R0 " bitop3:0x96\n\t"                                   \
                      "v_bitop3_b32 %1, %6, %7, " R1 " bitop3:0x96\n\t"                                    \
@@ -787,7 +708,7 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     }
 #define JL_G(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - JL_RING_SLACK) : "memory");                         \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P_ - JL_RING_SLACK) : "memory");                         \
         if (ce > e0 && ce + 1u < cE) {                                                                     \
             JL_XS4(R0, R1, R2, R3)                                                                         \
         } else {                                                                                           \
@@ -814,13 +735,12 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     // fewer entries from the fast path (rounds of 32 entries: ~72 % fast vs ~47 %).
 #define JL_F(u, RQ, R0, R1, R2, R3)                                                                        \
     {                                                                                                      \
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VAR == 1 ? 0 : P_ - JL_RING_SLACK) : "memory");                         \
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P_ - JL_RING_SLACK) : "memory");                         \
         JL_XS4(R0, R1, R2, R3)                                                                             \
         JL_GLD(RQ, pf.addr, 128 * ((u) & 3), R0, R1, R2, R3)                                               \
     }
-    const bool fast_ok = !DBG && VAR != 5;  // debugging / study variants: per-entry path only
 #define JL_HALF(SLOTS)                                                                                     \
-    if (fast_ok && ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E) {             \
+    if (ce > e0 && ce + 4u < cE && pf.r < pf.R && pf.e >= e0 && pf.e + 4u < pf.E) {             \
         SLOTS(JL_F)                                                                                        \
         ce = uni(ce + 4u);                                                                                 \
         pf.e = uni(pf.e + 4u);                                                                             \
@@ -828,25 +748,9 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
     } else {                                                                                               \
         SLOTS(JL_G)                                                                                        \
     }
-    if constexpr (VAR == 3) {  // study: whole 8-entry fast turns only
-        for (;;) {
-            if (fast_ok && ce > e0 && ce + (uint32_t)P_ < cE && pf.r < pf.R && pf.e >= e0 &&
-                pf.e + (uint32_t)P_ < pf.E) {
-                JL_GV4_SLOTS_LO(JL_F)
-                pf.addr += 512u;
-                JL_GV4_SLOTS_HI(JL_F)
-                ce = uni(ce + (uint32_t)P_);
-                pf.e = uni(pf.e + (uint32_t)P_);
-                pf.addr += 512u;
-                continue;
-            }
-            JL_GV4_SLOTS(JL_G)
-        }
-    } else {
-        for (;;) {
-            JL_HALF(JL_GV4_SLOTS_LO)
-            JL_HALF(JL_GV4_SLOTS_HI)
-        }
+    for (;;) {
+        JL_HALF(JL_GV4_SLOTS_LO)
+        JL_HALF(JL_GV4_SLOTS_HI)
     }
 #undef JL_HALF
 #undef JL_F
@@ -856,65 +760,10 @@ __global__ __launch_bounds__(JL_GV4_THREADS) void crc_gv4_kernel(const uint4 *__
 #undef JL_LOAD
 #undef JL_GLD
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring drains before the wave ends
-#if JL_GV4_WAVETIME
-    if (lane == 0 && w < 16384u) {
-        JL_WT_ARR[2u * w] = wt0;
-        JL_WT_ARR[2u * w + 1u] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
 }
-
-}  // namespace jlk
-
-#if JL_GV4_WAVETIME
-// study builds: per wave [start, end] of the last crc_gv4_kernel launch of this mode (and clear them)
-extern "C" int JL_WT_CAT(jl_study_gv4_wavetime_m, JL_MODE)(unsigned long long *out) {
-    static unsigned long long zero[2 * 16384];
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(jlk::JL_WT_ARR), sizeof(zero)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(jlk::JL_WT_ARR), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
-}
-#endif
-
-namespace jlk {
 
 template <>
 hipError_t launch_gv4_m<JL_MODE>(const void *img, const GV4Args &A, const uint8_t *zero, int grid, hipStream_t st) {
-#if JL_STUDY
-    // study variants: 1 = vmcnt(0) before every ring use, 4 = address checks,
-    // 5 = per-entry path only, 3 = whole 8-entry fast turns, 2 = no nt policy,
-    // 6 = no step math (memory side), 7 = L2-resident data (math side)
-    if (A.study) {
-        const int v = A.study;
-        if (v == 1)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 1>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 4)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 4>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 5)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 5>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 3)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 3>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 6)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 6>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 7)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 7>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 8)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 8>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else if (v == 9)
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 9>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        else
-            hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE, 2>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img,
-                               A, zero);
-        return hipGetLastError();
-    }
-#endif
     hipLaunchKernelGGL((crc_gv4_kernel<JL_MODE>), dim3(grid), dim3(JL_GV4_THREADS), 0, st, (const uint4 *)img, A, zero);
     return hipGetLastError();
 }

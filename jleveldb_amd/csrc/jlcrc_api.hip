@@ -229,7 +229,7 @@ constexpr int64_t kHostThresholdDefault = 4 << 20, kLogHostThresholdDefault = 16
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
 // batch takes and its tuning.  Defaults are the measured best; tests force the
-// alternatives.  The study options exist in the study build only (make STUDY=1).
+// alternatives.
 struct Options {
     int general_path = JL_PATH_AUTO;  // JL_OPT_GENERAL_PATH
     int stream_depth = 16;            // JL_OPT_STREAM_DEPTH: 16 / 32 / 48 ring entries
@@ -240,7 +240,7 @@ struct Options {
     int64_t stage_piece = 16 << 20;   // JL_OPT_STAGE_PIECE: staged copy pieces of big chunks (0: whole chunk)
     int64_t host_threshold = kHostThresholdDefault;  // JL_OPT_HOST_THRESHOLD: smaller host-memory calls run on the host
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
-    int gv4_variant = 0;              // study: JL_OPT_GV4_VARIANT (0 = the product kernel)
+    int failpoint = 0;                // JL_OPT_FAILPOINT (tests): bit 0 perturbs lc_dwalk's offsets
 };
 Options &opt() {
     static Options o;
@@ -532,7 +532,13 @@ int no_capture(void *stream, const char *who) {
     const hipError_t e = hipStreamIsCapturing(pick(stream), &cs);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        return fail(JL_ERR_INVALID, std::string(who) + ": stream capture (HIP graphs) is not supported (" +
+        // the null (legacy) stream while ANOTHER stream captures in global mode: the
+        // given stream itself is not capturing, but work on it would join that capture
+        if (e == hipErrorStreamCaptureImplicit)
+            return fail(JL_ERR_INVALID, std::string(who) +
+                                            ": the null stream cannot be used while another stream is being captured "
+                                            "into a HIP graph (global capture mode); pass a stream of your own");
+        return fail(JL_ERR_INVALID, std::string(who) + ": the stream's capture status cannot be queried (" +
                                         hipGetErrorString(e) + ")");
     }
     if (cs != hipStreamCaptureStatusNone)
@@ -634,7 +640,6 @@ static int run_gv4(const jlk::KParams &P, hipStream_t st) {
     memset(&A, 0, sizeof(A));
     A.P = P;
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
-    A.study = (uint32_t)opt().gv4_variant;
     // blocks above kGSplitMin (MODE_CRC) are split into chunks folded afterwards
     const bool can_split = P.mode == jlk::MODE_CRC;
     if (!P.off && ((uintptr_t)P.base & 127) == 0 && (P.fixed_bytes & 127) == 0 &&
@@ -767,12 +772,10 @@ int jl_set_option(int option, int64_t value) {
         if (value < 0) break;
         o.log_host_threshold = value;
         return JL_OK;
-#if JL_STUDY
-    case JL_OPT_GV4_VARIANT:
-        if (value < 0 || value > 9) break;
-        o.gv4_variant = (int)value;
+    case JL_OPT_FAILPOINT:
+        if (value < 0 || value > 1) break;
+        o.failpoint = (int)value;
         return JL_OK;
-#endif
     default:
         return fail(JL_ERR_INVALID, "jl_set_option: unknown option " + std::to_string(option));
     }
@@ -791,7 +794,7 @@ int64_t jl_get_option(int option) {
     case JL_OPT_HOST_THRESHOLD: return o.host_threshold;
     case JL_OPT_LOG_HOST_THRESHOLD: return o.log_host_threshold;
     case JL_OPT_STAGE_PIECE: return o.stage_piece;
-    case JL_OPT_GV4_VARIANT: return o.gv4_variant;
+    case JL_OPT_FAILPOINT: return o.failpoint;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
     }
 }
@@ -1354,6 +1357,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // lc_dense of the other half: random lengths 2.64 -> 2.47 ms, but every other
     // set 3-5 % slower (the cross-stream waits and the extra launches, ~40 us)
     JL_HIP(jlk::launch_lc_dwalk(A, st));
+    if (opt().failpoint & 1) JL_HIP(jlk::launch_lc_failpoint(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:
@@ -1381,7 +1385,6 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
         G.deal = A.dense_ctr + 2;  // zero when the verification starts (lc_finish of the one before)
         G.seed0 = jlmath::slice4_inv(0xffffffffu);
         G.parts = A.parts;
-        G.study = (uint32_t)opt().gv4_variant;  // 0 unless a study build set JL_OPT_GV4_VARIANT
         JL_HIP(gv4_launch(G, st));
         JL_HIP(jlk::launch_lc_combine(A, st));
         JL_HIP(jlk::launch_lc_apply(A, st));
@@ -1394,7 +1397,13 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     JL_HIP(poll_stream(st));
     const volatile uint64_t *hr = c.h_res;
     const uint64_t res[3] = {hr[0], hr[1], hr[2]};
-    if (res[2]) return fail(JL_ERR_HIP, "jl_log_verify: internal capacity exceeded");
+    if (res[2]) {
+        if (res[2] & jlk::kLCFlagStale) c.lc_dirty = true;  // the next call zeroes the counters itself
+        return fail(JL_ERR_HIP, std::string("jl_log_verify: ") +
+                                    (res[2] & jlk::kLCFlagStale ? "work counters not reset by the previous verification"
+                                     : res[2] & jlk::kLCFlagInconsistent ? "records of a block overlap"
+                                                                        : "internal capacity exceeded"));
+    }
     *n_events = res[0];
     return JL_OK;
 }

@@ -75,7 +75,6 @@ struct GV4Args {
     const uint32_t *n_rounds;   // device count of rounds (sorted pipeline)
     uint32_t seed0;             // W for init 0 = slice4^-1(0xffffffff)
     uint32_t fixed_K;           // implicit rounds (128-B aligned base and stride: no pads)
-    uint32_t study;             // study build only: crc_gv4_kernel variant (0 = the product kernel)
     uint32_t *parts;            // split blocks: raw chunk states (group idx = kGPart | part index)
     uint32_t *deal;             // rounds counter, zero at launch (null: each workgroup deals its own)
 };
@@ -196,6 +195,14 @@ hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
 hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
+// cap_flag bits (result word 2): a capacity of the round table / multi-chunk records
+// exceeded; records of one dense block that overlap (more long records than slots);
+// the work counters were not zero when lc_walk started (an earlier verification of
+// this workspace stopped before lc_finish)
+constexpr uint32_t kLCFlagCapacity = 1u, kLCFlagInconsistent = 2u, kLCFlagStale = 4u;
+// JL_OPT_FAILPOINT (tests): lc_dwalk's offsets of the listed dense blocks
+// perturbed before lc_dense reads them (each of lc_dense's consistency checks hit)
+hipError_t launch_lc_failpoint(const LCArgs &A, hipStream_t st);
 // lc_dwalk: header offsets kept per dense block; a run of kDWRun equal records
 // ends its walk (lc_dense's trips measure runs 257 records at a time)
 constexpr uint32_t kDWMax = 512;

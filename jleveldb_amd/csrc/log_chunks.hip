@@ -181,7 +181,11 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     const uint64_t b = (uint64_t)wg * 256u + threadIdx.x;
     if (b == 0) {
         A.count[A.n_blocks] = 0;
-        *A.cap_flag = 0;
+        // the work counters later kernels take ids from must be zero (lc_finish of the
+        // verification before re-zeroes them; the host memsets them after a call that
+        // stopped early): stale ones would start lc_dense / gv4 / lc_scan past their
+        // work, so they are reported instead
+        *A.cap_flag = (A.dense_ctr[1] | A.dense_ctr[2] | A.dense_ctr[3]) ? kLCFlagStale : 0u;
         *A.stash_ctr = 0;
     }
     uint32_t cnt = 0;
@@ -426,7 +430,7 @@ __global__ __launch_bounds__(kLCBins) void lc_setup_kernel(LCArgs A) {
     if (k == 0) {
         const bool over = total > A.round_cap;
         A.rstart[kLCBins] = over ? (uint32_t)A.round_cap : total;
-        if (over) atomicOr(A.cap_flag, 1u);
+        if (over) atomicOr(A.cap_flag, kLCFlagCapacity);
     }
     const uint64_t r = (uint64_t)ex + cnt / 8u;
     if (cnt & 7u) {
@@ -478,7 +482,7 @@ __device__ __forceinline__ void lc_place_wave(const LCArgs &A, uint32_t *ctr, co
             big.J = g.J;
             A.big[bi] = big;
         } else {
-            atomicOr(A.cap_flag, 1u);
+            atomicOr(A.cap_flag, kLCFlagCapacity);
             if (bi < A.big_cap) A.big[bi].J = 0u;  // skipped by lc_combine
         }
     }
@@ -800,6 +804,33 @@ __global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
     A.dw_info[b] = n | (p << 16);
 }
 
+// JL_OPT_FAILPOINT (tests only): lc_dwalk's results of the listed blocks it walked,
+// perturbed one way per list index mod 6, so that each consistency check of
+// lc_dense's first pass meets offsets that disagree with the block's bytes:
+// 0 an inner offset one byte off, 1 more offsets than kDWMax, 2 the resume position
+// one byte off, 3 the first offset not 0, 4 the last offset past the block, 5 none.
+__global__ __launch_bounds__(256) void lc_failpoint_kernel(LCArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.dense_ctr[0]) return;
+    const uint32_t e = A.dense_list[i];
+    if (e & kDWUniform) return;
+    const uint64_t b = e;
+    const uint32_t info = A.dw_info[b], n = info & 0xffffu;
+    uint16_t *o = A.dw_off + b * kDWMax;
+    switch (i % 6u) {
+    case 0: if (n >= 2u) o[n / 2u] = (uint16_t)(o[n / 2u] + 1u); break;
+    case 1: A.dw_info[b] = (info & 0xffff0000u) | (kDWMax + 1u); break;
+    case 2: A.dw_info[b] = info + (1u << 16); break;
+    case 3: if (n) o[0] = 7u; break;
+    case 4: if (n) o[n - 1u] = 32765u; break;
+    default: break;
+    }
+}
+hipError_t launch_lc_failpoint(const LCArgs &A, hipStream_t st) {
+    hipLaunchKernelGGL(lc_failpoint_kernel, dim3((A.n_blocks + 255u) / 256u), dim3(256), 0, st, A);
+    return hipGetLastError();
+}
+
 constexpr uint32_t kLDThreads = 256;
 __device__ __forceinline__ uint32_t lds32u(const uint32_t *d, uint32_t p) {  // bytes p..p+3, any alignment
     return __builtin_amdgcn_alignbyte(d[(p >> 2) + 1u], d[p >> 2], p & 3u);
@@ -964,6 +995,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ unsigned long long s_seg;  // stash offset of the pass's segment (~0: did not fit)
     __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
     __shared__ uint32_t doff[kDWMax / 2];  // lc_dwalk's header offsets of the block (u16 pairs)
+    __shared__ uint32_t s_inc;            // lc_dwalk's offsets disagree with the staged bytes
     const uint32_t nd = uni(A.dense_ctr[0]);
     uint32_t *const ctr = &A.dense_ctr[1];  // list entries taken
     if (nd == 0) return;  // no dense block in the log
@@ -1042,6 +1074,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             // a 194-record run went unreported, test_dense_list_in_chunks_random_lengths)
             if (bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
             s_bad = kLCNone;
+            s_inc = 0;
         }
         bp = b;
         ld_sync();
@@ -1058,8 +1091,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
-        const uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each)
-        uint32_t dc = 0;                       // uniform: offsets taken
+        uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each; 0 once found inconsistent)
+        uint32_t dc = 0;                 // uniform: offsets taken
         uint64_t seg0 = ~0ull;      // uniform: the block's first segment (stash offset | entries << 48)
         uint64_t link = ~0ull;      // uniform: the previous segment's link slot
         bool fit = true, done = false;
@@ -1068,7 +1101,13 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
             const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
             if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
-                const uint32_t k = atomicAdd(&A.nlong[b], 1u);  // < kLCSlots: >= 513 B each
+                // < kLCSlots for records of one chain (>= 513 B each); more would mean
+                // records that overlap: reported (cap_flag), never a write past the slots
+                const uint32_t k = atomicAdd(&A.nlong[b], 1u);
+                if (k >= kLCSlots) {
+                    atomicOr(A.cap_flag, kLCFlagInconsistent);
+                    return;
+                }
                 A.slots[b * kLCSlots + k] = (uint64_t)h | ((uint64_t)len << 16) | ((uint64_t)lds32u(dat, h) << 32);
                 lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
                 return;
@@ -1129,21 +1168,41 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 // DBBench's blocks).  Bucket 32 - G (G <= 32; long records, deferred
                 // to the rounds: bucket 32, last).
                 const uint32_t m = dn;
-                dc = dn;
-                p = dinfo >> 16;  // the block's rest: the walk below, from where lc_dwalk stopped
+                const uint32_t resume = dinfo >> 16;
+                // lc_dwalk's offsets are trusted only as the chain the staged bytes
+                // give: offset 0 first, every record OK (rem >= 7 + len, not type 0 of
+                // length 0) and followed by the next offset (the last by the resume
+                // position).  Offsets that disagree (r5: a study build read different
+                // bytes in the two kernels; lc_dense then checked garbage ranges and
+                // wrote long-record slots past the block's, an aperture violation in
+                // crc_gv4) leave the block to this kernel's own walk from its start.
+                bool bad = m > kDWMax;
                 uint32_t bk[2] = {0u, 0u}, rk[2] = {0u, 0u};
-                if (crc) {
 #pragma unroll
-                    for (uint32_t i = 0; i < 2; i++) {
-                        const uint32_t r = t + 256u * i;
-                        if (r < m) {
-                            const uint32_t h = doff16(r), len = (lds32u(dat, h + 3u) >> 8) & 0xffffu;
+                for (uint32_t i = 0; i < 2; i++) {
+                    const uint32_t r = t + 256u * i;
+                    if (!bad && r < m) {
+                        const uint32_t h = doff16(r), nx = r + 1u < m ? doff16(r + 1u) : resume;
+                        bad = (r == 0u && h != 0u) || blen < 7u || h > blen - 7u || nx > blen;
+                        const uint32_t key = bad ? 0u : lds32u(dat, h + 3u) >> 8, len = key & 0xffffu;
+                        bad = bad || key == 0u || h + 7u + len != nx;
+                        if (crc && !bad) {
                             const uint32_t dw = ((h + 10u + len) >> 2) - ((h + 6u) >> 2);  // nd of check()
                             bk[i] = dw > kLDLongDw ? 32u : 32u - ((dw + 3u) >> 2);
                             rk[i] = atomicAdd(&run_b[bk[i]], 1u);
                         }
                     }
-                    ld_sync();
+                }
+                if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) atomicOr(&s_inc, 1u);
+                ld_sync();
+                if (uni(s_inc)) {  // the whole block through the walk passes below (run_b is theirs again)
+                    dn = dc = 0;
+                    p = 0;
+                    continue;
+                }
+                dc = dn;
+                p = resume;  // the block's rest: the walk below, from where lc_dwalk stopped
+                if (crc) {
                     if (t < 64u) {  // bucket starts, after the 33 counts
                         const uint32_t v = t <= 32u ? run_b[t] : 0u;
                         const uint32_t ex = lc_wave_excl_sum(v);

@@ -28,9 +28,8 @@ def asm(tmp_path_factory):
     def one(i):
         src, defs = UNITS[i]
         out = d / f"u{i}.s"
-        # the study build: the product kernels and the gv4 bound-study variants
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-pass-failed",
-                        "--cuda-device-only", "-S", "-DJL_STUDY=1", *defs, "-o", str(out), os.path.join(CSRC, src)],
+                        "--cuda-device-only", "-S", *defs, "-o", str(out), os.path.join(CSRC, src)],
                        check=True, capture_output=True)
         return out.read_text()
 

@@ -125,3 +125,27 @@ def test_long_and_short_failures_in_one_dense_block(gpu, jl, oracle):
             log[int(after["offset"][0]) + 7 + 60] ^= 0x02
     w = _check(jl, oracle, log)
     assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= len(cases)
+
+
+@pytest.mark.parametrize("maxlen", [40, 200, 800])
+def test_inconsistent_dwalk_offsets_recovered(gpu, jl, oracle, maxlen):
+    """lc_dense trusts lc_dwalk's header offsets only as the chain its staged
+    bytes give (offsets that disagreed made it check garbage
+    ranges and write long-record slots past the block's, an aperture fault in
+    crc_gv4).  JL_OPT_FAILPOINT perturbs the offsets of every listed block five
+    ways (an inner offset, the count past kDWMax, the resume position, the first
+    offset, the last offset past the block); every such block must be re-walked
+    by lc_dense itself: events equal the oracle's, flips included, no fault."""
+    rng = np.random.default_rng(SEED + 7 * maxlen)
+    lens = rng.integers(0, maxlen + 1, (48 << 20) // (maxlen // 2 + 7)).astype(np.uint32)
+    log = _log(jl, gpu, lens)
+    nb = log.numel() >> 15
+    for b in (2, 5, nb // 2, nb - 4):  # flips in a few blocks' records
+        log[(b << 15) + 3000] ^= 0x10
+    prev = jl.set_option(jl.OPT_FAILPOINT, 1)
+    try:
+        w = _check(jl, oracle, log)
+    finally:
+        jl.set_option(jl.OPT_FAILPOINT, prev)
+    assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= 1
+    _check(jl, oracle, log)  # and the same log without the failpoint

@@ -254,6 +254,42 @@ def test_stream_capture_refused(gpu, jl, oracle, log_image):
                           _live(oracle.log_events(log_image[: 8 << 20])))
 
 
+def test_null_stream_during_global_capture(gpu, jl):
+    """A device entry point called on the NULL (legacy) stream while another
+    stream captures in global mode: the NULL stream itself is not capturing.
+    With torch's non-blocking capture stream HIP lets the call run (the NULL
+    stream does not synchronise with it): the results are right and the other
+    stream's capture goes on.  Where HIP reports the implicit capture instead
+    (hipErrorStreamCaptureImplicit) the call is refused with its own message,
+    nothing is enqueued.  Either way the graph replays what it captured."""
+    import ctypes
+    import torch
+
+    data = torch.zeros(4 * 4096, dtype=torch.uint8, device=gpu)
+    jl.fill_random_dev(data, 11)
+    want = jl.crc32c_fixed_dev(data, 4096).clone()
+    out = torch.zeros(4, dtype=torch.int32, device=gpu)
+    x = torch.arange(16, dtype=torch.float32, device=gpu)
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):  # torch's default capture mode: global
+        y = x * 2.0
+        rc = jl.lib().jl_crc32c_fixed_dev(data.data_ptr(), 4096, 4, jl.FLAG_MASK, out.data_ptr(), ctypes.c_void_p(0))
+        msg = jl.lib().jl_last_error().decode()
+        y = y + 1.0
+    torch.cuda.synchronize()
+    if rc == 0:
+        assert torch.equal(out, want)
+    else:
+        assert rc == -1 and "null stream" in msg, (rc, msg)
+        assert int(out.abs().sum()) == 0  # nothing ran
+    x.copy_(torch.arange(16, dtype=torch.float32, device=gpu) + 1.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(y, (torch.arange(16, dtype=torch.float32, device=gpu) + 1.0) * 2.0 + 1.0)
+
+
 @pytest.mark.parametrize("mode", ["staged", "pinned"])
 def test_dense_log_host(gpu, jl, oracle, engine_options, mode):
     """~150 MiB DBBench-default log (131-B payloads: every 32 KiB block dense) with

@@ -16,8 +16,6 @@ torch.cuda.set_device(0)
 jl.init(0)
 jl.set_option(jl.OPT_GENERAL_PATH, {"auto": jl.PATH_AUTO, "stream": jl.PATH_STREAM,
                                     "gv4": jl.PATH_GV4}[os.environ.get("C3_PATH", "auto")])
-if os.environ.get("GV4_VARIANT"):  # study build (JLCRC_STUDY_LIB): 6 = no step math, 7 = L2-resident data
-    jl.set_option(jl.OPT_GV4_VARIANT, int(os.environ["GV4_VARIANT"]))
 dev = torch.device("cuda:0")
 rng = np.random.default_rng(SEED)
 n = int(os.environ.get("C3_N", 1 << 20))

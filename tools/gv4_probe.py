@@ -7,8 +7,8 @@ the 4 KiB kernel (fixed_v4) on the same bytes.  Times, on one 4 GiB arena:
   sorted    1M x 4 KiB through jl_crc32c_batch_dev (offsets: gv4 rounds pipeline,
             round descriptors)
   ceiling   jl_read_stream_dev over the arena
-With JLCRC_STUDY_LIB=<study build> and GV4_VARIANT=6 the gv4 legs run without
-step math (memory side only), =7 on L2-resident data (math side only)."""
+(The gv4 bound-study variants this probe drove in r3, GV4_VARIANT=6 / 7, live on
+the branch study-r5-gv4-switches.)"""
 import json
 import os
 import sys
@@ -21,8 +21,6 @@ import jleveldb_amd as jl  # noqa: E402
 
 torch.cuda.set_device(0)
 jl.init(0)
-if os.environ.get("GV4_VARIANT"):
-    jl.set_option(jl.OPT_GV4_VARIANT, int(os.environ["GV4_VARIANT"]))
 dev = torch.device("cuda:0")
 n = 1 << 20
 data = torch.empty(n * 4096 + 4096, dtype=torch.uint8, device=dev)
@@ -51,4 +49,4 @@ for name, fn in legs.items():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 10
     res[name] = {"ms": round(ms, 4), "TB_per_s": round(n * 4096 / ms / 1e9, 3)}
-print(json.dumps({"variant": os.environ.get("GV4_VARIANT", "0"), **res}), flush=True)
+print(json.dumps(res), flush=True)

@@ -8,8 +8,8 @@ at ~6.7).  Same 4 GiB arena, blocks of ~1 KiB, one leg per layout:
   log_1057       1057-B blocks at a 1063-B stride (the C5 record crc ranges: K = 9/10, every tail pad)
   implicit_4224  4224-B blocks at a 4224-B stride (implicit rounds of K = 33)
   fixed4k        1M x 4 KiB through the 4 KiB kernel (reference)
-LEGS=a,b selects legs; GV4_VARIANT=v with JLCRC_STUDY_LIB=<study build> runs a
-study variant of the gv4 kernel (general_v4.hip VAR).
+LEGS=a,b selects legs (the gv4 study variants it ran in r3 live on the branch
+study-r5-gv4-switches).
 Run under rocprofv3 --kernel-trace --stats: the gv4 kernel's own time per leg
 is in the trace (legs run in this order, 20 launches each)."""
 import json
@@ -24,8 +24,6 @@ import jleveldb_amd as jl  # noqa: E402
 
 torch.cuda.set_device(0)
 jl.init(0)
-if os.environ.get("GV4_VARIANT"):  # study build (JLCRC_STUDY_LIB): general_v4.hip VAR
-    jl.set_option(jl.OPT_GV4_VARIANT, int(os.environ["GV4_VARIANT"]))
 dev = torch.device("cuda:0")
 size = 4 << 30
 data = torch.empty(size + 8192, dtype=torch.uint8, device=dev)

@@ -17,8 +17,6 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 which = sys.argv[2] if len(sys.argv) > 2 else "all"
 torch.cuda.set_device(0)
 jl.init(0)
-if os.environ.get("GV4_VARIANT"):  # study build (JLCRC_STUDY_LIB): general_v4.hip VAR
-    jl.set_option(jl.OPT_GV4_VARIANT, int(os.environ["GV4_VARIANT"]))
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream()
 if which == "all" or "c3" in which.split(","):
