@@ -102,16 +102,23 @@ const char *jl_version(void);
  *                            engine while the host copies the next piece (a
  *                            chunk of <= 4 pieces' worth goes in 4 MiB pieces;
  *                            0 = one piece per chunk).  Default 16 MiB
- *   JL_OPT_HOST_THRESHOLD    host-memory entry points jl_crc32c_fixed / _batch and
- *                            jl_table_verify: a call touching fewer bytes than
- *                            this runs on the calling thread's SSE4.2 path
- *                            (bit-identical; no device work; a device must still
- *                            be present); 0 = always the device.  Default 4 MiB,
- *                            the crossover of the per-call latencies on the
- *                            round-end driver's boxes (one table)
+ *   JL_OPT_HOST_THRESHOLD    host-memory entry points jl_crc32c_fixed / _batch,
+ *                            jl_table_verify and jl_tables_verify: a call touching
+ *                            fewer bytes than this runs on the calling thread's
+ *                            SSE4.2 path (bit-identical; no device work; a device
+ *                            must still be present); 0 = always the device.
+ *                            Default JL_HOST_THRESHOLD_AUTO (-1): the engine
+ *                            measures both paths per size class (2^17 .. 2^28 B)
+ *                            on this box and sends each call to the faster one
+ *                            (below 128 KiB always the host, from 256 MiB always
+ *                            the device)
  *   JL_OPT_LOG_HOST_THRESHOLD  the same for jl_log_verify (and jl_log_read_records);
- *                            default 16 MiB (the driver's crossover; one ~4 MiB
- *                            WAL stays on the host)
+ *                            default JL_HOST_THRESHOLD_AUTO
+ *   JL_OPT_LOG_SMALL_MAX     log verification: a log (or a 64 MiB chunk of a
+ *                            host-memory log) of at most this many bytes is
+ *                            verified in one launch, one workgroup per 32 KiB
+ *                            block; larger ones take the chunked path (walk,
+ *                            rounds).  0 = always the chunked path.  Default 16 MiB
  *   JL_OPT_FAILPOINT         tests only: bit 0 perturbs the dense blocks' header
  *                            offsets between lc_dwalk and lc_dense (a different
  *                            inconsistency per block); results must not change
@@ -127,6 +134,21 @@ const char *jl_version(void);
 #define JL_OPT_LOG_HOST_THRESHOLD 8
 #define JL_OPT_STAGE_PIECE 9
 #define JL_OPT_FAILPOINT 10
+#define JL_OPT_LOG_SMALL_MAX 11
+#define JL_HOST_THRESHOLD_AUTO (-1)
+/* Read-only (jl_get_option; jl_set_option refuses them): the staging copy pool
+ * and the calling thread's last host-memory call, for diagnostics.
+ *   JL_INFO_STAGE_WORKERS         copy-pool threads running
+ *   JL_INFO_STAGE_SPAWN_FAILURES  copy-pool threads that could not be started
+ *   JL_INFO_LAST_PATH             0 = the host path, 1 = the device, -1 = none yet
+ *   JL_INFO_LAST_CALL_NS          its wall time
+ *   JL_INFO_LAST_STAGE_NS         the part spent copying pageable input into
+ *                                 pinned staging (0 when DMA'd directly) */
+#define JL_INFO_STAGE_WORKERS 201
+#define JL_INFO_STAGE_SPAWN_FAILURES 202
+#define JL_INFO_LAST_PATH 203
+#define JL_INFO_LAST_CALL_NS 204
+#define JL_INFO_LAST_STAGE_NS 205
 #define JL_PATH_AUTO 0
 #define JL_PATH_STREAM 1
 #define JL_PATH_GV4 2
@@ -272,9 +294,10 @@ int jl_log_verify_dev(const void *d_log, uint64_t log_bytes, int checksum, jl_lo
  * the kernels are enqueued on `stream`; the result words land in device memory
  * d_result[3] in stream order: [0] the event total (events past `cap` are not
  * written: the events are complete when [0] <= cap, for any log), [1] the
- * number of dense blocks (more than 64 records; informational), [2] non-zero if
- * an internal capacity was exceeded (cannot happen; reported rather than
- * assumed).  checksum: JL_LOG_NO_CHECKSUM,
+ * number of dense blocks the chunked path verified whole (more than 64 records;
+ * informational; 0 on the one-launch path of logs up to JL_OPT_LOG_SMALL_MAX),
+ * [2] non-zero if an internal capacity was exceeded or the scratch was not in the
+ * state the call expects (cannot happen; reported rather than assumed).  checksum: JL_LOG_NO_CHECKSUM,
  * JL_LOG_CHECKSUM or JL_LOG_CHECKSUM_TWO_PASS.  A thread's log calls share its
  * scratch: a later call on another stream (the null stream included) first makes
  * its stream wait for this one (device-side).  Lets a caller

@@ -213,6 +213,9 @@ OPT_GENERAL_PATH, OPT_STREAM_DEPTH, OPT_STREAM_PARTITION, OPT_SPLIT_CAP = 1, 2, 
 OPT_HOST_REGISTER, OPT_STAGE_THREADS, OPT_HOST_THRESHOLD, OPT_LOG_HOST_THRESHOLD = 5, 6, 7, 8
 OPT_STAGE_PIECE = 9
 OPT_FAILPOINT = 10  # tests only
+OPT_LOG_SMALL_MAX = 11
+HOST_THRESHOLD_AUTO = -1
+INFO_STAGE_WORKERS, INFO_STAGE_SPAWN_FAILURES, INFO_LAST_PATH, INFO_LAST_CALL_NS, INFO_LAST_STAGE_NS = 201, 202, 203, 204, 205
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2
 
 
@@ -490,8 +493,8 @@ def log_verify_dev(log, checksum: bool = True, events=None, stream=None):
 def log_verify_dev_async(log, checksum: bool = True, events=None, result=None, stream=None):
     """Asynchronous device-resident verification (jl_log_verify_dev_async): enqueues
     the kernels and returns (events, result) at once; result (3 x int64 on the
-    device, filled in stream order) = [events, dense blocks (informational),
-    internal-capacity flag]; the events are complete for any log when [0] <= the
+    device, filled in stream order) = [events, dense blocks of the chunked path
+    (informational; 0 on the one-launch small-log path), internal-capacity flag]; the events are complete for any log when [0] <= the
     events capacity."""
     import torch
 

@@ -38,14 +38,20 @@ class CopyPool {
             std::unique_lock<std::mutex> lk(mu_);
             // a thread that cannot be started (rlimit, a container's pid limit) must
             // not throw through the C ABI: the copy goes on with the threads running
-            // (the caller alone if there are none), and no later call retries
-            while (!spawn_failed_ && (int)th_.size() < threads - 1 && (int)th_.size() < 63) {
+            // (the caller alone if there are none); the spawn is retried at most once
+            // a second, and the failures are counted (JL_INFO_STAGE_SPAWN_FAILURES)
+            const auto now = std::chrono::steady_clock::now();
+            if (failures_ && now - last_fail_ < std::chrono::seconds(1)) threads = (int)th_.size() + 1;
+            while ((int)th_.size() < threads - 1 && (int)th_.size() < 63) {
                 try {
                     th_.emplace_back([this] { work(); });
                 } catch (...) {
-                    spawn_failed_ = true;
+                    failures_++;
+                    last_fail_ = now;
+                    break;
                 }
             }
+            live_.store((int)th_.size());
             q_.push_back(&j);
             queued_.fetch_add(1);
         }
@@ -59,6 +65,11 @@ class CopyPool {
             q_.erase(it);
             queued_.fetch_sub(1);
         }
+    }
+    int workers() const { return live_.load(); }  // threads running
+    int spawn_failures() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return failures_;
     }
     ~CopyPool() {
         {
@@ -120,6 +131,8 @@ class CopyPool {
     std::atomic<int> queued_{0};  // jobs in q_ (read by spinning workers without the lock)
     std::vector<std::thread> th_;
     bool stop_ = false;
-    bool spawn_failed_ = false;  // guarded by mu_
+    int failures_ = 0;                                // threads that could not start (guarded by mu_)
+    std::chrono::steady_clock::time_point last_fail_;  // guarded by mu_
+    std::atomic<int> live_{0};                        // th_.size(), readable without the lock
 };
 }  // namespace jlhost

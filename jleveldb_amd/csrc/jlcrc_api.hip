@@ -77,13 +77,14 @@ struct DevBuf {
 struct PinBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;  // hipHostMallocCoherent: written by kernels, read by the host
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         size_t want = std::max<size_t>(bytes, 4096);
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, flags);
         if (e == hipSuccess) cap = want;
         return e;
     }
@@ -115,6 +116,12 @@ struct Workspace {
     hipStream_t stream = nullptr;  // compute stream of the host-memory entry points
     DevBuf ws_lc, ws_slot, ws_desc, ws_big, ws_part, ws_tmp, ws_stash;  // chunked log verify (log_chunks.hip)
     DevBuf ws_ls, ws_lsev;  // fused log verify: per-block counts / first failures, event slots
+    DevBuf ws_small;        // one-launch small-log verify (lc_small): ticket counter, look-back statuses
+    // jl_log_verify of a small log: lc_small writes the events here (fine-grained
+    // pinned memory: its stores reach host memory, none waits in the GPU's L2)
+    PinBuf h_ev{nullptr, 0, hipHostMallocCoherent};
+    uint32_t small_gen = 0;   // the last lc_small call's status tag
+    bool small_dirty = true;  // ws_small not known to hold a zero ticket counter (new buffer, failed call)
     // the chunked log verify's result words: coherent host memory the last kernel
     // writes directly (no D2H copy of them, the host polls the stream)
     uint64_t *h_res = nullptr;
@@ -137,8 +144,10 @@ struct Workspace {
         async_done = nullptr;
         if (h_res) (void)hipHostFree(h_res);
         h_res = nullptr;
-        for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_stash, &ws_ls, &ws_lsev})
+        for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_stash, &ws_ls, &ws_lsev, &ws_small})
             b->release();
+        small_dirty = true;
+        h_ev.release();
         for (Slot &sl : slot) {
             if (sl.st) (void)hipStreamSynchronize(sl.st);
             for (DevBuf *b : {&sl.d_in, &sl.d_desc, &sl.d_out}) b->release();
@@ -211,21 +220,20 @@ int get_ws(Workspace **out) {
     return JL_OK;
 }
 
-// Host-memory calls touching fewer bytes than these run on the calling thread's
-// SSE4.2 path (host_paths.cpp): below them the device round trip (copies,
-// launches, synchronisation) costs more than the CRC itself.  The defaults are
-// the crossovers the round-end driver measured on fresh boxes (bench.py
-// "dispatch", BENCH_r03 / BENCH_r04, pageable input, one caller): a table of
-// ~4.2 KB blocks costs the device 156 us against the host's 146 at 2 MiB and 229
-// against 288 at 4 MiB; a WAL of 1 056-B records 591 against 514 us at 8 MiB and
-// 713 against 810 at 16 MiB.  Our own sessions measure the device ~20 % faster
-// at 2-16 MiB (r5f, a fresh box, dispatch first in its process: 122 vs 147 us
-// at 2 MiB, 486 vs 517 at 8 MiB; 64 MiB agrees everywhere), so the lower
-// crossovers (2 / 8 MiB) did not hold on the driver's boxes; at 4 / 16 MiB the
-// device is faster on every box measured.  jleveldb's 2 MiB tables
-// (Options.java:208) and ~4 MiB WALs (Options.java:203) therefore take the host
-// path; a compaction's input tables (jl_tables_verify) and larger logs the device.
-constexpr int64_t kHostThresholdDefault = 4 << 20, kLogHostThresholdDefault = 16 << 20;
+// Host-memory calls run either on the calling thread's SSE4.2 path
+// (host_paths.cpp) or on the device; below a few MiB the device round trip
+// (staging copy, DMA, launches, synchronisation) can cost more than the CRC
+// itself.  Where the two cross depends on the box: the round-end driver's boxes
+// staged pageable input at a third of our sessions' rate (BENCH_r05: a 16 MiB
+// table 1 140 vs 505 us on the device, the same 1 180 vs 1 150 us on the host),
+// so no fixed size is right everywhere.  The default (JL_HOST_THRESHOLD_AUTO)
+// measures instead: per kind of call and size class the first calls run once or
+// twice on each path, then every call takes the faster one, and one call in 32
+// re-measures the other (Dispatch below).  A threshold >= 0 fixes the split.
+constexpr int64_t kHostThresholdDefault = JL_HOST_THRESHOLD_AUTO, kLogHostThresholdDefault = JL_HOST_THRESHOLD_AUTO;
+// Logs (and host-pipeline chunks of logs) up to this size take the one-launch path
+// (lc_small_kernel: one workgroup per 32 KiB block); larger ones the chunked path.
+constexpr int64_t kLogSmallMaxDefault = 16 << 20;
 
 // Engine options (jl_set_option, include/jlcrc.h): which general-path kernel a
 // batch takes and its tuning.  Defaults are the measured best; tests force the
@@ -241,11 +249,77 @@ struct Options {
     int64_t host_threshold = kHostThresholdDefault;  // JL_OPT_HOST_THRESHOLD: smaller host-memory calls run on the host
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
     int failpoint = 0;                // JL_OPT_FAILPOINT (tests): bit 0 perturbs lc_dwalk's offsets
+    int64_t log_small_max = kLogSmallMaxDefault;  // JL_OPT_LOG_SMALL_MAX: logs up to this size verify in one launch
 };
 Options &opt() {
     static Options o;
     return o;
 }
+
+// ------------------------------------------------------------ call dispatch
+// Auto dispatch state: per kind of call (blocks: crc batches and tables; logs)
+// and size class (2^17 .. 2^28 bytes), the two paths' recent cost per byte.
+constexpr int kKindBlocks = 0, kKindLog = 1, kDispBuckets = 12, kDispExplore = 32;
+constexpr uint64_t kDispHostBelow = 128u << 10;    // auto: always the host below this
+constexpr uint64_t kDispDeviceFrom = 256ull << 20;  // auto: always the device from this
+struct Dispatch {
+    struct Cell {
+        double ns_per_byte[2] = {0.0, 0.0};  // [0] host path, [1] device path
+        uint32_t n[2] = {0u, 0u};             // calls measured
+        uint32_t calls = 0;
+    };
+    std::mutex mu;
+    Cell cell[2][kDispBuckets];
+};
+Dispatch &dispatch() {
+    static Dispatch d;
+    return d;
+}
+// the calling thread's last host-memory call (JL_INFO_*)
+thread_local int t_last_path = -1;
+thread_local int64_t t_last_ns = 0, t_stage_ns = 0;
+
+// The route of one host-memory call: its path (threshold >= 0: fixed; auto: the
+// measured costs), its time recorded for the auto dispatch once it succeeded.
+struct Route {
+    int kind, bucket = -1;
+    uint64_t bytes;
+    bool host = false, ok = false;
+    std::chrono::steady_clock::time_point t0;
+    Route(int k, uint64_t b, int64_t threshold) : kind(k), bytes(b), t0(std::chrono::steady_clock::now()) {
+        t_stage_ns = 0;
+        if (threshold >= 0) {
+            host = (int64_t)b < threshold;
+        } else if (b < kDispHostBelow || b >= kDispDeviceFrom) {
+            host = b < kDispHostBelow;
+        } else {
+            bucket = std::min(kDispBuckets - 1, 63 - __builtin_clzll(b) - 17);
+            Dispatch &D = dispatch();
+            std::lock_guard<std::mutex> lk(D.mu);
+            Dispatch::Cell &c = D.cell[kind][bucket];
+            c.calls++;
+            if (c.n[1] < 2) host = false;       // measure the device path (the first call is a cold one)
+            else if (c.n[0] < 2) host = true;   // then the host path
+            else host = (c.ns_per_byte[0] <= c.ns_per_byte[1]) != (c.calls % kDispExplore == 0);
+        }
+        t_last_path = host ? 0 : 1;
+    }
+    ~Route() {
+        const int64_t ns =
+            std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        t_last_ns = ns;
+        if (bucket < 0 || !ok || bytes == 0) return;
+        Dispatch &D = dispatch();
+        std::lock_guard<std::mutex> lk(D.mu);
+        Dispatch::Cell &c = D.cell[kind][bucket];
+        const int p = host ? 0 : 1;
+        const double v = (double)ns / (double)bytes;
+        // the first measurement of a path in a class is replaced by the second (first-use
+        // allocations, cold pages), later ones enter an average that follows drift
+        c.ns_per_byte[p] = c.n[p] < 2 ? v : 0.75 * c.ns_per_byte[p] + 0.25 * v;
+        c.n[p]++;
+    }
+};
 
 // Initialises the engine on device 0 if no jl_init came first, and binds the
 // calling thread to the engine's device (HIP's current device is per thread).
@@ -341,7 +415,11 @@ jlhost::CopyPool &copy_pool() {
     static jlhost::CopyPool *p = new jlhost::CopyPool;  // never destroyed: workers may outlive static destruction order
     return *p;
 }
-void par_memcpy(void *dst, const void *src, size_t n) { copy_pool().copy(dst, src, n, std::max(1, opt().stage_threads)); }
+void par_memcpy(void *dst, const void *src, size_t n) {
+    const auto t0 = std::chrono::steady_clock::now();
+    copy_pool().copy(dst, src, n, std::max(1, opt().stage_threads));
+    t_stage_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
 
 // Enqueues the copy of src.p[off, off + bytes) into sl.d_in on the slot's copy
 // stream, after the slot's previous use; staged through pinned memory when the
@@ -761,7 +839,7 @@ int jl_set_option(int option, int64_t value) {
         o.stage_threads = (int)value;
         return JL_OK;
     case JL_OPT_HOST_THRESHOLD:
-        if (value < 0) break;
+        if (value < JL_HOST_THRESHOLD_AUTO) break;
         o.host_threshold = value;
         return JL_OK;
     case JL_OPT_STAGE_PIECE:
@@ -769,12 +847,16 @@ int jl_set_option(int option, int64_t value) {
         o.stage_piece = value;
         return JL_OK;
     case JL_OPT_LOG_HOST_THRESHOLD:
-        if (value < 0) break;
+        if (value < JL_HOST_THRESHOLD_AUTO) break;
         o.log_host_threshold = value;
         return JL_OK;
     case JL_OPT_FAILPOINT:
         if (value < 0 || value > 1) break;
         o.failpoint = (int)value;
+        return JL_OK;
+    case JL_OPT_LOG_SMALL_MAX:
+        if (value < 0 || value > (int64_t)JL_STREAM_CHUNK_BYTES) break;
+        o.log_small_max = value;
         return JL_OK;
     default:
         return fail(JL_ERR_INVALID, "jl_set_option: unknown option " + std::to_string(option));
@@ -795,6 +877,12 @@ int64_t jl_get_option(int option) {
     case JL_OPT_LOG_HOST_THRESHOLD: return o.log_host_threshold;
     case JL_OPT_STAGE_PIECE: return o.stage_piece;
     case JL_OPT_FAILPOINT: return o.failpoint;
+    case JL_OPT_LOG_SMALL_MAX: return o.log_small_max;
+    case JL_INFO_STAGE_WORKERS: return copy_pool().workers();
+    case JL_INFO_STAGE_SPAWN_FAILURES: return copy_pool().spawn_failures();
+    case JL_INFO_LAST_PATH: return t_last_path;
+    case JL_INFO_LAST_CALL_NS: return t_last_ns;
+    case JL_INFO_LAST_STAGE_NS: return t_stage_ns;
     default: return fail(JL_ERR_INVALID, "jl_get_option: unknown option " + std::to_string(option));
     }
 }
@@ -914,8 +1002,10 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     if (n_blocks == 0) return JL_OK;
     if (!host || !out || block_bytes == 0) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: bad arguments");
     if (block_bytes > JL_STREAM_CHUNK_BYTES) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: block larger than a chunk");
-    if ((int64_t)(n_blocks * block_bytes) < opt().host_threshold) {  // a small call: host SSE4.2 path
+    Route rt(kKindBlocks, n_blocks * block_bytes, opt().host_threshold);
+    if (rt.host) {  // the host SSE4.2 path
         jlhost::fixed(host, block_bytes, n_blocks, flags, out);
+        rt.ok = true;
         return JL_OK;
     }
     Workspace *w = nullptr;
@@ -928,7 +1018,7 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     }
     HostSrc src(host, n_blocks * block_bytes);
     const uint64_t n_chunks = (n_blocks + per - 1) / per;
-    return pipeline(
+    const int rc = pipeline(
         *w, n_chunks,
         [&](uint64_t i, Slot &sl) {
             return slot_put_data(sl, src, i * per * block_bytes, std::min(per, n_blocks - i * per) * block_bytes);
@@ -940,6 +1030,8 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
             JL_HIP(hipMemcpyAsync(out + b0, sl.d_out.p, nb * 4, hipMemcpyDeviceToHost, w->stream));
             return JL_OK;
         });
+    rt.ok = rc == JL_OK;
+    return rc;
 }
 
 int jl_crc32c_batch_dev(const void *d_base, uint64_t base_bytes, const uint64_t *d_off, const uint32_t *d_len,
@@ -971,8 +1063,10 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
             return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
         touched += len[i];
     }
-    if ((int64_t)touched < opt().host_threshold) {  // a small call: host SSE4.2 path
+    Route rt(kKindBlocks, touched, opt().host_threshold);
+    if (rt.host) {  // the host SSE4.2 path
         jlhost::batch(base, off, len, init, suffix, n, flags, out);
+        rt.ok = true;
         return JL_OK;
     }
     Workspace *w = nullptr;
@@ -980,7 +1074,7 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
     const std::vector<Chunk> ch = plan_chunks(off, len, 0, n);
     if (int r = ensure_chunk_bufs(*w, ch, 4, 8 + 4 + 4 + 1)) return r;
     HostSrc src(base, base_bytes);
-    return pipeline(
+    const int rc = pipeline(
         *w, ch.size(),
         [&](uint64_t i, Slot &sl) -> int {
             const Chunk &k = ch[i];
@@ -1005,6 +1099,8 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
             JL_HIP(hipMemcpyAsync(out + k.a, sl.d_out.p, m * 4, hipMemcpyDeviceToHost, w->stream));
             return JL_OK;
         });
+    rt.ok = rc == JL_OK;
+    return rc;
 }
 
 // ------------------------------------------------------------- table shims
@@ -1048,8 +1144,10 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
             return fail(JL_ERR_INVALID, "jl_table_verify: truncated block read");  // TableFormat.java:203-206
         touched += (uint64_t)size[i] + 5;
     }
-    if ((int64_t)touched < opt().host_threshold) {  // a small call (one table): host SSE4.2 path
+    Route rt(kKindBlocks, touched, opt().host_threshold);
+    if (rt.host) {  // the host SSE4.2 path (one table)
         jlhost::table_verify(file, off, size, n, status);
+        rt.ok = true;
         return JL_OK;
     }
     Workspace *w = nullptr;
@@ -1057,7 +1155,7 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
     const std::vector<Chunk> ch = plan_chunks(off, size, 5, n);  // block || 5-byte trailer
     if (int r = ensure_chunk_bufs(*w, ch, 1, 8 + 4)) return r;
     HostSrc src(file, file_bytes);
-    return pipeline(
+    const int rc = pipeline(
         *w, ch.size(),
         [&](uint64_t i, Slot &sl) -> int {
             const Chunk &k = ch[i];
@@ -1078,6 +1176,8 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
             JL_HIP(hipMemcpyAsync(status + k.a, sl.d_out.p, m, hipMemcpyDeviceToHost, w->stream));
             return JL_OK;
         });
+    rt.ok = rc == JL_OK;
+    return rc;
 }
 
 // The input tables of a compaction verified together (VersionSet.makeInputIterator
@@ -1108,9 +1208,11 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
         }
     }
     if (n == 0) return JL_OK;
-    if ((int64_t)touched < opt().host_threshold) {
+    Route rt(kKindBlocks, touched, opt().host_threshold);
+    if (rt.host) {
         for (uint64_t t = 0; t < n_tables; t++)
             jlhost::table_verify(files[t], off + first[t], size + first[t], first[t + 1] - first[t], status + first[t]);
+        rt.ok = true;
         return JL_OK;
     }
     // groups of whole tables (a table larger than a chunk is a group of its own)
@@ -1140,7 +1242,7 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
         JL_HIP(sl.d_desc.ensure(max_h * 12 + 4 * 256));
     }
     std::vector<uint64_t> adj;
-    return pipeline(
+    const int rc = pipeline(
         *w, groups.size(),
         [&](uint64_t gi, Slot &sl) -> int {
             const Group &g = groups[gi];
@@ -1170,6 +1272,8 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
             JL_HIP(hipMemcpyAsync(status + h0, sl.d_out.p, m, hipMemcpyDeviceToHost, w->stream));
             return JL_OK;
         });
+    rt.ok = rc == JL_OK;
+    return rc;
 }
 
 // --------------------------------------------------------------- log shims
@@ -1408,6 +1512,47 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     return JL_OK;
 }
 
+// One-launch verification of a small log (lc_small_kernel, log_chunks.hip):
+// d_result null: synchronous (the count read back from the result words the
+// kernel writes into coherent host memory); else asynchronous.
+static int log_verify_small(Workspace &c, const void *d_log, uint64_t log_bytes, bool checksum, jl_log_event *d_events,
+                            uint64_t cap, uint64_t *n_events, hipStream_t st, uint64_t *d_result = nullptr) {
+    // (d_events may be pinned host memory: jl_log_verify's small-log path)
+    const uint64_t nb = (log_bytes + 32767) / 32768;
+    const size_t cap0 = c.ws_small.cap;
+    JL_HIP(c.ws_small.ensure(256 + nb * 8));
+    if (c.ws_small.cap != cap0) c.small_dirty = true;
+    // a zero ticket counter and statuses that no tag matches: zero once per buffer
+    // (the statuses then carry each call's tag, the last ticket re-zeroes the counter)
+    if (c.small_dirty) JL_HIP(hipMemsetAsync(c.ws_small.p, 0, c.ws_small.cap, st));
+    c.small_dirty = true;  // until the launch is enqueued
+    if (++c.small_gen == 0) c.small_gen = 1;
+    if (!c.h_res) JL_HIP(hipHostMalloc((void **)&c.h_res, 64, hipHostMallocCoherent));
+    jlk::LSmallArgs A;
+    memset(&A, 0, sizeof(A));
+    A.log = (const uint8_t *)d_log;
+    A.size = log_bytes;
+    A.n_blocks = (uint32_t)nb;
+    A.checksum = checksum ? 1 : 0;
+    A.seed0 = jlmath::slice4_inv(0xffffffffu);
+    A.gen = c.small_gen;
+    A.aux = ctx().d_aux;
+    A.ev = (jlk::LogEvent *)d_events;
+    A.ev_cap = d_events ? cap : 0;
+    A.ticket = (uint32_t *)c.ws_small.p;
+    A.tstat = (uint64_t *)((char *)c.ws_small.p + 256);
+    A.result = d_result ? d_result : c.h_res;
+    JL_HIP(jlk::launch_lc_small(A, st));
+    c.small_dirty = false;
+    if (d_result) return JL_OK;
+    JL_HIP(poll_stream(st));
+    *n_events = ((const volatile uint64_t *)c.h_res)[0];
+    return JL_OK;
+}
+static bool small_log(uint64_t log_bytes, int checksum) {
+    return checksum != JL_LOG_CHECKSUM_FUSED && (int64_t)log_bytes <= opt().log_small_max;
+}
+
 // Verifies d_log[0, log_bytes) on `st` with the calling thread's scratch `c`;
 // *n_events is known on return (the event count is read back) and the events
 // are complete in stream order.
@@ -1422,8 +1567,13 @@ static int log_verify_impl(Workspace &c, const void *d_log, uint64_t log_bytes, 
     }
     *n_events = 0;
     if (log_bytes == 0) return JL_OK;
-    if (int r = log_verify_chunks(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, n_events, st))
+    if (small_log(log_bytes, checksum)) {
+        if (int r = log_verify_small(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, n_events, st))
+            return r;
+    } else if (int r = log_verify_chunks(c, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, n_events,
+                                         st)) {
         return r;
+    }
     if (*n_events > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
     return JL_OK;
 }
@@ -1481,9 +1631,43 @@ int jl_log_verify_dev_async(const void *d_log, uint64_t log_bytes, int checksum,
         return JL_OK;
     }
     uint64_t n = 0;
+    const bool cs = checksum != JL_LOG_NO_CHECKSUM;
     return ws_after(*w, st, true,
-                    log_verify_chunks(*w, d_log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, d_events, cap, &n, st,
-                                      d_result));
+                    small_log(log_bytes, checksum) ? log_verify_small(*w, d_log, log_bytes, cs, d_events, cap, &n, st, d_result)
+                                                   : log_verify_chunks(*w, d_log, log_bytes, cs, d_events, cap, &n, st, d_result));
+}
+
+// A small host-memory log (at most JL_OPT_LOG_SMALL_MAX): one H2D copy (staged in
+// kStagePiece pieces, each DMA'd as soon as it is in pinned memory; 1 / 2 MiB
+// pieces measured no better, same box, r6g), one lc_small launch that
+// writes the events straight into pinned host memory, one wait, one host copy of
+// the events into the caller's array.  The chunked pipeline below costs this
+// call a second round trip (the event rebase and D2H after the count is known).
+static int log_verify_small_host(Workspace &w, const uint8_t *log, uint64_t log_bytes, bool checksum, jl_log_event *events,
+                                 uint64_t cap, uint64_t *n_events) {
+    Slot &sl = w.slot[0];
+    const uint64_t ev_max = log_bytes / 7 + 2;  // physical records of the log, at most
+    JL_HIP(sl.d_in.ensure(log_bytes + kSlack));
+    JL_HIP(w.h_ev.ensure(ev_max * sizeof(jl_log_event)));
+    HostSrc src(log, log_bytes);
+    if (src.direct) {
+        JL_HIP(hipMemcpyAsync(sl.d_in.p, log, log_bytes, hipMemcpyHostToDevice, w.stream));
+    } else {
+        JL_HIP(sl.h_data.ensure(log_bytes));
+        for (uint64_t a = 0; a < log_bytes; a += kStagePiece) {
+            const uint64_t m = std::min(kStagePiece, log_bytes - a);
+            par_memcpy((uint8_t *)sl.h_data.p + a, log + a, m);
+            JL_HIP(hipMemcpyAsync((uint8_t *)sl.d_in.p + a, (const uint8_t *)sl.h_data.p + a, m, hipMemcpyHostToDevice,
+                                  w.stream));
+        }
+    }
+    uint64_t n = 0;
+    if (int r = log_verify_small(w, sl.d_in.p, log_bytes, checksum, (jl_log_event *)w.h_ev.p, ev_max, &n, w.stream))
+        return r;
+    *n_events = n;
+    if (n > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    par_memcpy(events, w.h_ev.p, n * sizeof(jl_log_event));
+    return JL_OK;
 }
 
 // Host-memory log verification: chunks of JL_STREAM_CHUNK_BYTES (whole 32 KiB
@@ -1498,14 +1682,23 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     static_assert(JL_STREAM_CHUNK_BYTES % 32768 == 0, "log chunks must be whole blocks");
     *n_events = 0;
     if (log_bytes == 0) return JL_OK;
-    if ((int64_t)log_bytes < opt().log_host_threshold) {  // a small log (one WAL at recovery): host SSE4.2 path
+    Route rt(kKindLog, log_bytes, opt().log_host_threshold);
+    if (rt.host) {  // the host SSE4.2 path (e.g. one WAL at recovery)
         jlhost::log_verify(log, log_bytes, checksum, events, cap, n_events);
         if (*n_events > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+        rt.ok = true;
         return JL_OK;
     }
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     if (int r = ws_order(*w, w->stream)) return r;
+    if (small_log(log_bytes, checksum)) {
+        const int rc = log_verify_small_host(*w, log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, events, cap, n_events);
+        if (rc) (void)hipStreamSynchronize(w->stream);  // nothing of the call left in flight
+        w->async_pending = false;  // w->stream waited for any earlier asynchronous call, and it is done
+        rt.ok = rc == JL_OK;
+        return rc;
+    }
     const uint64_t CH = JL_STREAM_CHUNK_BYTES, first = std::min(CH, log_bytes);
     const uint64_t ev_cap = first / 7 + 2;  // upper bound on a chunk's physical records
     for (Slot &sl : w->slot) {
@@ -1555,6 +1748,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     w->async_pending = false;  // the pipeline drained this thread's streams after any earlier async call
     if (rc) return rc;
     if (total > cap) return fail(JL_ERR_CAPACITY, "jl_log_verify: event array too small");
+    rt.ok = true;
     return JL_OK;
 }
 

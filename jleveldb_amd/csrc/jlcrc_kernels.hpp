@@ -195,6 +195,31 @@ hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
 hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
+// Small logs in one launch (lc_small_kernel, log_chunks.hip): one workgroup per
+// 32 KiB block (the blocks in ticket order) stages the block in LDS, walks it
+// (readPhysicalRecord's decisions), checks every OK record's crc there (one
+// thread per record, one wave per record of more than kLDLongDw dwords), takes
+// its first event's place from a decoupled look-back over the earlier blocks'
+// event counts and writes its events in file order: no scans, rounds or host
+// round trip.  Scratch: the ticket counter (zero between calls: the last ticket's
+// taker re-zeroes it) and one look-back status per block, tagged with the call's
+// generation `gen` (statuses of earlier calls never match: no memset per call).
+struct LSmallArgs {
+    const uint8_t *log;
+    uint64_t size;
+    uint32_t n_blocks;
+    int checksum;
+    uint32_t seed0;          // slice4^-1(0xffffffff)
+    uint32_t gen;            // this call's status tag (never 0)
+    const uint32_t *aux;     // T0 and the z^L nibble tables (lc_zshift)
+    LogEvent *ev;
+    uint64_t ev_cap;
+    uint32_t *ticket;
+    uint64_t *tstat;         // n_blocks look-back statuses: gen << 32 | kLSInc / kLSAgg | events
+    uint64_t *result;        // [0] events, [1] 0, [2] 0 (written by the last block's workgroup)
+};
+constexpr uint64_t kLSInc = 1ull << 31, kLSAgg = 1ull << 30, kLSVal = kLSAgg - 1;
+hipError_t launch_lc_small(const LSmallArgs &A, hipStream_t st);
 // cap_flag bits (result word 2): a capacity of the round table / multi-chunk records
 // exceeded; records of one dense block that overlap (more long records than slots);
 // the work counters were not zero when lc_walk started (an earlier verification of

@@ -866,6 +866,60 @@ __device__ __forceinline__ uint32_t ld_z1(const uint32_t *T0, uint32_t s) { retu
 // z^-1(s) through Ti[b] = (T0[i] << 8) | i, i the byte whose T0 entry has top byte b
 // (z(r) = (r >> 8) ^ T0[r & 0xff] keeps T0's top byte, a permutation of i)
 __device__ __forceinline__ uint32_t ld_zi1(const uint32_t *Ti, uint32_t s) { return (s << 8) ^ Ti[s >> 24]; }
+// The crc tables of lc_dense / lc_small (LDS): N4 / N8 the 5-bit tables of z^4 / z^8
+// (ld_map), Ti the inverse byte table (ld_zi1), W0 value()'s seed word and C_h =
+// z^4(W0 << 8h) (a crc range starting h bytes into a dword)
+struct LDTabs {
+    const uint32_t *N4, *N8, *Ti;
+    uint32_t W0, C1, C2, C3;
+};
+// One OK record's crc from the staged block dat (header at h, payload length len,
+// crc range [h + 6, h + 7 + len) of at most kLDLongDw + 1 dwords): true when it
+// equals the stored crc.  One thread per record.
+__device__ __forceinline__ bool ld_crc_ok(const uint32_t *dat, const LDTabs &T, uint32_t h, uint32_t len) {
+    const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
+    const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+    // the record's last dword is read whole: its 4 - tl bytes past the record
+    // (the next header's) enter the chains' result s linearly, as themselves
+    // (the last dword is chain 1's last word, XORed in unshifted), so s is
+    // compared with want ^ those bytes instead of masking the dword in the loop
+    const uint32_t gmask = tl ? ~((1u << (8u * tl)) - 1u) : 0u;
+    // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last dword
+    // was padded with 4 - tl zeros (tl = 0: the state): so u = z^-tl(stored
+    // state), tl = 0: z^-4 (inverse byte steps, ahead of the chains, so their
+    // dependent lookups overlap the chains'; one z^4 fold of 7 lookups less)
+    uint32_t want = ~unmask_crc(lds32u(dat, h));
+    for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(T.Ti, want);
+    want ^= dat[a + nd - 1u] & gmask;
+    // the first dword, seeded (C_h folds in the seed dword before it)
+    const uint32_t d = dat[a];
+    uint32_t x0 = ~d;
+    if (hq) {
+        const uint32_t c = hq == 1u ? T.C1 : (hq == 2u ? T.C2 : T.C3);
+        x0 = c ^ ((T.W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+    }
+    // two chains: the record's dwords end-aligned on pairs (o zero dwords in
+    // front), chain c takes position c of every pair and steps z^8; at the
+    // end chain 0 still owes z^4.  r4 ran four chains stepping z^16 and
+    // folded them with z^12 / z^8 / z^4 (21 lookups per record against 7):
+    // the crc phase is bound by the CU's LDS pipe and VALU issue together,
+    // not by latency, so the fold's lookups cost more than the ILP gained
+    // (r5l, same box: DBBench 1.274 -> 1.242 ms, random lengths 2.643 ->
+    // 2.602).  Issuing both chains' 14 lookups together (the compiler
+    // waits for chain 0's before reusing its registers for chain 1's
+    // addresses) was no faster either (r5n: 1.264 vs 1.255 ms)
+    const uint32_t o = nd & 1u, G = (nd + o) >> 1;
+    const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
+    uint32_t y0 = o ? 0u : x0, y1 = o ? x0 : D[1];
+    for (uint32_t g = 1; g < G; g++) {
+        const uint32_t v0 = D[2u * g], v1 = D[2u * g + 1u];
+        y0 = ld_map(T.N8, y0, v0);
+        y1 = ld_map(T.N8, y1, v1);
+    }
+    const uint32_t sv = ld_map(T.N4, y0, y1);
+    return sv == want;
+}
+
 // A workgroup's dense blocks come from lc_walk's list (dense_list[0 .. dense_ctr[0])),
 // kLDChunk entries at a time from the counter dense_ctr[1], so a workgroup that
 // runs faster takes more blocks (r4; r3 dealt the blocks statically,
@@ -1026,6 +1080,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
     const uint32_t W0 = A.seed0;
     const uint32_t C1 = ld_map(N4, W0 << 8), C2 = ld_map(N4, W0 << 16), C3 = ld_map(N4, W0 << 24);
+    const LDTabs T{N4, N8, t0, W0, C1, C2, C3};
     LDSched sch;
     sch.nd = nd;
     sch.ch = ld_chunk(nd);
@@ -1099,7 +1154,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         // one OK record's crc (header at h, payload length len) against its stored crc
         auto check = [&](uint32_t h, uint32_t len) {
             const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
-            const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+            const uint32_t nd = ((e + 3u) >> 2) - (q >> 2);
             if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
                 // < kLCSlots for records of one chain (>= 513 B each); more would mean
                 // records that overlap: reported (cap_flag), never a write past the slots
@@ -1112,45 +1167,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
                 return;
             }
-            // the record's last dword is read whole: its 4 - tl bytes past the record
-            // (the next header's) enter the chains' result s linearly, as themselves
-            // (the last dword is chain 1's last word, XORed in unshifted), so s is
-            // compared with want ^ those bytes instead of masking the dword in the loop
-            const uint32_t gmask = tl ? ~((1u << (8u * tl)) - 1u) : 0u;
-            // the chains end as u with z^4(u) = z^(4 - tl)(state) when the last dword
-            // was padded with 4 - tl zeros (tl = 0: the state): so u = z^-tl(stored
-            // state), tl = 0: z^-4 (inverse byte steps, ahead of the chains, so their
-            // dependent lookups overlap the chains'; one z^4 fold of 7 lookups less)
-            uint32_t want = ~unmask_crc(lds32u(dat, h));
-            for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(t0, want);
-            want ^= dat[a + nd - 1u] & gmask;
-            // the first dword, seeded (C_h folds in the seed dword before it)
-            const uint32_t d = dat[a];
-            uint32_t x0 = ~d;
-            if (hq) {
-                const uint32_t c = hq == 1u ? C1 : (hq == 2u ? C2 : C3);
-                x0 = c ^ ((W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
-            }
-            // two chains: the record's dwords end-aligned on pairs (o zero dwords in
-            // front), chain c takes position c of every pair and steps z^8; at the
-            // end chain 0 still owes z^4.  r4 ran four chains stepping z^16 and
-            // folded them with z^12 / z^8 / z^4 (21 lookups per record against 7):
-            // the crc phase is bound by the CU's LDS pipe and VALU issue together,
-            // not by latency, so the fold's lookups cost more than the ILP gained
-            // (r5l, same box: DBBench 1.274 -> 1.242 ms, random lengths 2.643 ->
-            // 2.602).  Issuing both chains' 14 lookups together (the compiler
-            // waits for chain 0's before reusing its registers for chain 1's
-            // addresses) was no faster either (r5n: 1.264 vs 1.255 ms)
-            const uint32_t o = nd & 1u, G = (nd + o) >> 1;
-            const uint32_t *D = dat + a - o;  // D[j]: virtual dword j (j >= o)
-            uint32_t y0 = o ? 0u : x0, y1 = o ? x0 : D[1];
-            for (uint32_t g = 1; g < G; g++) {
-                const uint32_t v0 = D[2u * g], v1 = D[2u * g + 1u];
-                y0 = ld_map(N8, y0, v0);
-                y1 = ld_map(N8, y1, v1);
-            }
-            const uint32_t sv = ld_map(N4, y0, y1);
-            if (sv != want) atomicMin(&s_bad, h);
+            if (!ld_crc_ok(dat, T, h, len)) atomicMin(&s_bad, h);
         };
         auto doff16 = [&](uint32_t r) { return (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu; };
         while (!done) {
@@ -1353,6 +1370,296 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     }
     ld_sync();  // the last block's crc phase is done
     if (t == 0 && bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
+}
+
+
+// ---------------------------------------------------------------------------
+// lc_small: a small log (a WAL recovered at open, J/db/DBImpl.java:903; a
+// MANIFEST, J/db/VersionSet.java:487) verified in ONE launch (VERDICT r5 item 5:
+// the chunked path's ~11 dependent launches cost ~100 us even for a 0.25 MiB log).
+// One workgroup per 32 KiB block, blocks taken in ticket order (so a workgroup's
+// look-back only ever waits for workgroups that started before it):
+//   stage   the block into LDS (as lc_dense)
+//   walk    readPhysicalRecord's decisions in order (lc_dense's walk: runs of
+//           equal records measured 257 headers per trip); the first pass counts
+//           every event of the block and keeps up to kSRuns runs, a block of more
+//           runs is processed in further passes from where the kept runs end
+//   publish the block's event count (look-back status), before any crc work
+//   crc     one thread per OK record (ld_crc_ok), one wave per record of more than
+//           kLDLongDw dwords (ld_crc_wave_ok); the first failure's header offset
+//           (atomicMin) makes that record BAD_CRC and the later events of the
+//           block kind 0, as lc_apply does (J/db/LogReader.java:356-369)
+//   place   the block's first event = the earlier blocks' events (decoupled
+//           look-back by wave 0, 64 statuses per load), then the events in file
+//           order straight into the caller's array
+constexpr uint32_t kSRuns = 512;
+
+// One OK record of more than kLDLongDw dwords, by a whole wave: the record's
+// dwords end-aligned on 64 P virtual dwords (P = ceil(nd / 64); the zero dwords
+// in front leave a zero chain zero), lane i runs the chain over its P of them
+// (the first real dword seeded as in ld_crc_ok), then lane i's value is moved to
+// the record's end, z^(4 P (63 - i)) (lc_zshift, aux tables), and XOR-reduced.
+__device__ __forceinline__ bool ld_crc_wave_ok(const uint32_t *dat, const LDTabs &T, const uint32_t *aux, uint32_t h,
+                                               uint32_t len, uint32_t lane) {
+    const uint32_t q = h + 6u, e = h + 7u + len;
+    const uint32_t a = q >> 2, hq = q & 3u, nd = ((e + 3u) >> 2) - a, tl = e & 3u;
+    const uint32_t gmask = tl ? ~((1u << (8u * tl)) - 1u) : 0u;
+    uint32_t want = ~unmask_crc(lds32u(dat, h));
+    for (uint32_t z = tl ? tl : 4u; z; z--) want = ld_zi1(T.Ti, want);
+    want ^= dat[a + nd - 1u] & gmask;
+    const uint32_t d = dat[a];
+    uint32_t x0 = ~d;
+    if (hq) {
+        const uint32_t c = hq == 1u ? T.C1 : (hq == 2u ? T.C2 : T.C3);
+        x0 = c ^ ((T.W0 >> (32u - 8u * hq)) | (d & (~0u << (8u * hq))));
+    }
+    const uint32_t P = (nd + 63u) >> 6, front = 64u * P - nd;
+    uint32_t y = 0;
+    for (uint32_t j = 0; j < P; j++) {
+        const uint32_t v = lane * P + j;
+        const uint32_t k = v - front;
+        const uint32_t w = v < front ? 0u : (k ? dat[a + k] : x0);
+        y = ld_map(T.N4, y, w);
+    }
+    return wave_xor(lc_zshift(aux, y, 4u * P * (63u - lane))) == want;
+}
+
+__device__ __forceinline__ uint64_t ls_status(uint32_t gen, uint64_t flag, uint64_t v) {
+    return ((uint64_t)gen << 32) | flag | (v & kLSVal);
+}
+
+__global__ __launch_bounds__(kLDThreads) void lc_small_kernel(LSmallArgs A) {
+    __shared__ uint32_t dat[8192 + 4];         // the block (+ zero pad: header reads near its end)
+    __shared__ uint32_t nt[2 * kLDTabDwords];  // tables of z^4, z^8 (ld_map)
+    __shared__ uint32_t t0[256];               // T0, then the inverse byte table
+    __shared__ uint32_t run_a[kSRuns];         // offset in block | length << 16
+    __shared__ uint32_t run_b[kSRuns];         // first event (of the block) | type << 16 | kind << 24
+    __shared__ uint32_t lg[64];                // header offsets of the pass's long records
+    __shared__ uint32_t s_w[6];                // the walk's results (wave 0) for the other waves
+    __shared__ uint32_t s_bad, s_id;
+    __shared__ unsigned long long s_pre;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+    if (t == 0) {
+        s_id = atomicAdd(A.ticket, 1u);
+        if (s_id + 1u == A.n_blocks) *A.ticket = 0;  // every ticket taken: zero for the next call
+        s_bad = kLCNone;
+    }
+    t0[t] = A.aux[t];
+    ld_sync();
+    const uint64_t b = uni(s_id);
+    const uint64_t bs = b * 32768u;
+    const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+    const bool eof = blen < 32768u;
+    const bool vec = blen == 32768u && ((uintptr_t)(A.log + bs) & 15u) == 0;
+    LDPre pre;
+    if (vec) pre.load(A.log + bs, t);
+    for (uint32_t w = t; w < 2u * kLDTabDwords; w += kLDThreads) {  // as lc_dense
+        const uint32_t k = w / kLDTabDwords + 1u, e = w % kLDTabDwords;
+        const uint32_t i = e >> 5, v = e & 31u;
+        uint32_t x = i * 5u < 32u ? v << (5u * i) : 0u;
+        for (uint32_t z = 0; z < 4u * k; z++) x = ld_z1(t0, x);
+        nt[w] = x;
+    }
+    ld_sync();
+    {  // t0 becomes the inverse table (ld_zi1)
+        const uint32_t e = t0[t];
+        ld_sync();
+        t0[e >> 24] = (e << 8) | t;
+    }
+    if (vec) {
+        pre.store(dat, t);
+    } else {  // the log's short last block (or an unaligned log): bytes, nothing past its end
+        const uint8_t *src = A.log + bs;
+        for (uint32_t o = t; o < 8192u; o += kLDThreads) {
+            uint32_t v = 0;
+            for (uint32_t j = 0; j < 4; j++)
+                if (4u * o + j < blen) v |= (uint32_t)src[4u * o + j] << (8 * j);
+            dat[o] = v;
+        }
+    }
+    if (t < 4) dat[8192 + t] = 0;
+    ld_sync();
+    const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords;
+    const uint32_t W0 = A.seed0;
+    const LDTabs T{N4, N8, t0, W0, ld_map(N4, W0 << 8), ld_map(N4, W0 << 16), ld_map(N4, W0 << 24)};
+    auto longrec = [&](uint32_t h, uint32_t len) { return ((h + 10u + len) >> 2) - ((h + 6u) >> 2) > kLDLongDw; };
+    uint32_t p = 0, nev = 0;            // uniform: walk position, events walked so far
+    uint32_t total = 0;                 // uniform: the block's events (known after the first walk)
+    uint64_t start = 0;                 // uniform: the block's first event in the log
+    bool first = true;
+    for (;;) {
+        // ---- walk from p: up to kSRuns runs kept; the first pass counts on to the block's
+        // end.  Wave 0 alone walks (a chain of dependent LDS reads: the other waves'
+        // copies of it only queued in front of its reads, and its trips of 64
+        // candidates need no barrier); the others wait at the barrier below.
+        const uint32_t ev0 = nev;
+        if (wv == 0) {
+            uint32_t nr = 0, nl = 0, pk = ~0u, ev_end = 0, p_end = 0;
+            bool keep = true, more = false;
+            // kept runs go into lane nr mod 64 of va / vb (no exec-mask switch and no
+            // LDS store on the walk's chain), 64 at a time into LDS
+            uint32_t va = 0, vb = 0;
+            auto put = [&](uint32_t ra, uint32_t rb) {
+                const bool mine = lane == (nr & 63u);  // (a compare and two selects: no exec-mask switch)
+                va = mine ? ra : va;
+                vb = mine ? rb : vb;
+                if ((++nr & 63u) == 0u) {
+                    run_a[nr - 64u + lane] = va;
+                    run_b[nr - 64u + lane] = vb;
+                }
+            };
+            for (;;) {
+                const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
+                const bool okrec = rem >= 7u + len && key != 0u;  // lc_decide's kind 1: an OK record
+                if (okrec && key != pk && keep && nr < kSRuns && !longrec(p, len)) {
+                    // the common step (records of changing lengths): a new run of one
+                    put(p | (len << 16), nev | (w & 0xff000000u) >> 8 | (1u << 24));
+                    pk = key;
+                    nev++;
+                    p += 7u + len;
+                    continue;
+                }
+                if (okrec) {
+                    if (key == pk) {  // it repeats the record before it: lane l checks p + (l + 1) L
+                        const uint32_t L = 7u + len, c = p + (lane + 1u) * L;
+                        const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
+                        const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
+                        const uint32_t m = 1u + (nok ? (uint32_t)__builtin_ctzll(nok) : 64u);
+                        if (keep && longrec(p, len)) {  // < 64 records of > 512 B fit a block
+                            if (lane < m && nl + lane < 64u) lg[nl + lane] = p + lane * L;
+                            nl += m;
+                        }
+                        nev += m;
+                        p += m * L;
+                        continue;
+                    }
+                    if (keep && nr == kSRuns) {  // the first run not kept: a later pass starts here
+                        keep = false;
+                        more = true;
+                        p_end = p;
+                        ev_end = nev;
+                        if (!first) break;
+                    }
+                    if (keep) {
+                        if (longrec(p, len)) {
+                            if (lane == 0 && nl < 64u) lg[nl] = p;
+                            nl++;
+                        }
+                        put(p | (len << 16), nev | (w & 0xff000000u) >> 8 | (1u << 24));
+                    }
+                    pk = key;
+                    nev++;
+                    p += 7u + len;
+                    continue;
+                }
+                // the block's end: the trailer (no event) or a record that stops the walk
+                const LCDecision d0 = lc_decide(rem, eof, rem >= 7u ? w : 0u);
+                if (d0.kind != 0u) {
+                    if (keep && nr == kSRuns) {
+                        keep = false;
+                        more = true;
+                        p_end = p;
+                        ev_end = nev;
+                    }
+                    if (keep) put(p | (d0.length << 16), nev | (d0.type << 16) | (d0.kind << 24));
+                    nev++;
+                }
+                break;
+            }
+            if ((nr & 63u) != 0u && lane < (nr & 63u)) {  // the last, partial group of kept runs
+                run_a[(nr & ~63u) + lane] = va;
+                run_b[(nr & ~63u) + lane] = vb;
+            }
+            if (keep) ev_end = nev;
+            if (lane == 0) {
+                s_w[0] = nr;
+                s_w[1] = nl;
+                s_w[2] = nev;
+                s_w[3] = ev_end;
+                s_w[4] = p_end;
+                s_w[5] = more;
+                if (first)  // the block's event count, published before any crc work
+                    __hip_atomic_store(&A.tstat[b], ls_status(A.gen, b ? kLSAgg : kLSInc, nev), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        ld_sync();  // the pass's runs and long records are in LDS
+        const uint32_t nr = uni(s_w[0]), nl = uni(s_w[1]), ev_end = uni(s_w[3]), p_end = uni(s_w[4]);
+        const bool more = uni(s_w[5]) != 0u;
+        nev = uni(s_w[2]);
+        if (first) total = nev;
+        const uint32_t npass = ev_end - ev0;
+        if (A.checksum && uni(s_bad) == kLCNone) {  // (none once the block failed: the rest is dropped)
+            for (uint32_t r = t; r < npass; r += kLDThreads) {
+                uint32_t j = 0;  // the run holding event ev0 + r: the last with first <= it
+                for (uint32_t sh = nr > 1u ? 1u << (31 - __builtin_clz(nr - 1u)) : 0u; sh; sh >>= 1)
+                    if (j + sh < nr && (run_b[j + sh] & 0xffffu) <= ev0 + r) j += sh;
+                const uint32_t ra = run_a[j], rb = run_b[j];
+                if ((rb >> 24) != 1u) continue;
+                const uint32_t len = ra >> 16, h = (ra & 0xffffu) + (ev0 + r - (rb & 0xffffu)) * (7u + len);
+                if (longrec(h, len)) continue;  // the waves below
+                if (!ld_crc_ok(dat, T, h, len)) atomicMin(&s_bad, h);
+            }
+            for (uint32_t k = wv; k < nl && k < 64u; k += kLDThreads / 64u) {
+                const uint32_t h = lg[k], len = (lds32u(dat, h + 3u) >> 8) & 0xffffu;
+                if (!ld_crc_wave_ok(dat, T, A.aux, h, len, lane) && lane == 0) atomicMin(&s_bad, h);
+            }
+        }
+        if (first && wv == 0) {  // the block's first event: the events of the blocks before it
+            uint64_t prev = 0;
+            for (int64_t q = (int64_t)b - 1; q >= 0;) {
+                const int64_t i = q - (int64_t)lane;
+                const uint64_t st = i >= 0 ? __hip_atomic_load(&A.tstat[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                           : ls_status(A.gen, kLSInc, 0);
+                const bool ready = (uint32_t)(st >> 32) == A.gen && (st & (kLSInc | kLSAgg)) != 0;
+                const uint64_t im = __builtin_amdgcn_ballot_w64(ready && (st & kLSInc));
+                const uint32_t lim = im ? (uint32_t)__builtin_ctzll(im) : 63u;
+                const uint64_t need = lim == 63u ? ~0ull : (2ull << lim) - 1ull;
+                if ((__builtin_amdgcn_ballot_w64(ready) & need) != need) {  // a status not yet published
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const uint32_t v = lane <= lim ? (uint32_t)(st & kLSVal) : 0u;
+                prev += (uint32_t)__builtin_amdgcn_readlane((int)(lc_wave_excl_sum(v) + v), 63);
+                if (im) break;
+                q -= 64;
+            }
+            if (lane == 0) {
+                if (b) __hip_atomic_store(&A.tstat[b], ls_status(A.gen, kLSInc, prev + total), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                s_pre = prev;
+                if (b + 1u == A.n_blocks) {  // the last block: the result words
+                    A.result[0] = prev + total;
+                    A.result[1] = 0;
+                    A.result[2] = 0;
+                }
+            }
+        }
+        ld_sync();  // the crc phase's failures and the block's start
+        if (first) start = uni64(s_pre);
+        const uint32_t fb = uni(s_bad);
+        for (uint32_t r = t; r < npass; r += kLDThreads) {  // the pass's events, in file order
+            uint32_t j = 0;
+            for (uint32_t sh = nr > 1u ? 1u << (31 - __builtin_clz(nr - 1u)) : 0u; sh; sh >>= 1)
+                if (j + sh < nr && (run_b[j + sh] & 0xffffu) <= ev0 + r) j += sh;
+            const uint32_t ra = run_a[j], rb = run_b[j];
+            const uint32_t len = ra >> 16, h = (ra & 0xffffu) + (ev0 + r - (rb & 0xffffu)) * (7u + len);
+            uint32_t kind = rb >> 24;
+            if (A.checksum && fb != kLCNone) kind = h == fb ? 2u : (h > fb ? 0u : kind);
+            const uint64_t at = start + ev0 + r, off = bs + h;
+            if (at < A.ev_cap)
+                lc_st16(&A.ev[at], lc_v4{(uint32_t)off, (uint32_t)(off >> 32), len, ((rb >> 16) & 0xffu) | (kind << 8)});
+        }
+        if (!more) break;
+        ld_sync();  // the next pass rewrites the runs
+        p = p_end;
+        nev = ev_end;
+        first = false;
+    }
+}
+hipError_t launch_lc_small(const LSmallArgs &A, hipStream_t st) {
+    hipLaunchKernelGGL(lc_small_kernel, dim3(A.n_blocks), dim3(kLDThreads), 0, st, A);
+    return hipGetLastError();
 }
 
 // as many workgroups per CU as the LDS holds

@@ -58,6 +58,15 @@ def engine_options(jl):
         jl.set_option(option, value)
 
 
+@pytest.fixture(params=["small", "chunked"])
+def log_path(request, jl, engine_options):
+    """Runs a log test through both device paths: the one-launch small-log kernel
+    (lc_small, every log up to 64 MiB) and the chunked path (walk, dense blocks,
+    rounds) forced for every size (JL_OPT_LOG_SMALL_MAX = 0)."""
+    engine_options(jl.OPT_LOG_SMALL_MAX, (64 << 20) if request.param == "small" else 0)
+    return request.param
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

@@ -630,7 +630,8 @@ int main(int argc, char **argv) {
     const jlong thr0 = JFN(getOption)(env, NULL, JL_OPT_HOST_THRESHOLD);
     CHECK(JFN(setOption)(env, NULL, JL_OPT_HOST_THRESHOLD, 12345) == JL_OK &&
               JFN(getOption)(env, NULL, JL_OPT_HOST_THRESHOLD) == 12345, "setOption / getOption");
-    CHECK(JFN(setOption)(env, NULL, JL_OPT_LOG_HOST_THRESHOLD, -1) == JL_ERR_INVALID && g_exc[0] == 0, "bad option value");
+    CHECK(JFN(setOption)(env, NULL, JL_OPT_LOG_HOST_THRESHOLD, -2) == JL_ERR_INVALID && g_exc[0] == 0, "bad option value");
+    CHECK(JFN(setOption)(env, NULL, JL_OPT_LOG_HOST_THRESHOLD, JL_HOST_THRESHOLD_AUTO) == JL_OK, "auto threshold");
     CHECK(JFN(setOption)(env, NULL, JL_OPT_HOST_THRESHOLD, 0) == JL_OK, "threshold 0");
     CHECK(JFN(setOption)(env, NULL, JL_OPT_LOG_HOST_THRESHOLD, 0) == JL_OK, "log threshold 0");
     (void)thr0;

@@ -157,8 +157,9 @@ def test_options_round_trip_and_ranges(jl):
     cases = [  # option, valid values, invalid values
         (jl.OPT_HOST_REGISTER, [0, 1], [2, -1]),
         (jl.OPT_STAGE_THREADS, [1, 8, 64], [0, 65]),
-        (jl.OPT_HOST_THRESHOLD, [0, 2 << 20], [-1]),
-        (jl.OPT_LOG_HOST_THRESHOLD, [0, 8 << 20], [-1]),
+        (jl.OPT_HOST_THRESHOLD, [0, 2 << 20, jl.HOST_THRESHOLD_AUTO], [-2]),
+        (jl.OPT_LOG_HOST_THRESHOLD, [0, 8 << 20, jl.HOST_THRESHOLD_AUTO], [-2]),
+        (jl.OPT_LOG_SMALL_MAX, [0, 64 << 20, 16 << 20], [-1, (64 << 20) + 1]),
         (jl.OPT_STAGE_PIECE, [0, 1 << 20, 16 << 20], [-1, 4096]),
     ]
     for opt, good, bad in cases:

@@ -81,7 +81,40 @@ def test_threshold_option(jl, gpu, engine_options):
         engine_options(opt, 12345)
         assert jl.get_option(opt) == 12345
         with pytest.raises(jl.JLError):
-            jl.set_option(opt, -1)
+            jl.set_option(opt, -2)
+        for info in (jl.INFO_STAGE_WORKERS, jl.INFO_LAST_PATH):
+            with pytest.raises(jl.JLError):
+                jl.set_option(info, 0)
+
+
+@pytest.mark.parametrize("kind", ["table", "log"])
+def test_auto_dispatch(gpu, jl, oracle, engine_options, kind):
+    """JL_HOST_THRESHOLD_AUTO: in a size class the first calls run twice on each
+    path (JL_INFO_LAST_PATH shows which), every call's output is the same, and
+    once both are measured the calls keep to one path but for one in 32."""
+    rng = np.random.default_rng(SEED + 5)
+    if kind == "table":
+        data, offs, sizes = _table_file(oracle, rng, 1.5)
+        data[int(offs[3]) + 1] ^= 0x04
+        engine_options(jl.OPT_HOST_THRESHOLD, jl.HOST_THRESHOLD_AUTO)
+        run = lambda: jl.table_verify(data, offs, sizes)  # noqa: E731
+    else:
+        lens = wl.c5_lengths("c1_1056", target=3 << 20, seed=SEED)
+        src = rng.integers(0, 256, int(lens.sum(dtype=np.uint64)), dtype=np.uint8)
+        data = np.frombuffer(oracle.log_write([src[o:o + n].tobytes() for o, n in zip(wl.packed_offsets(lens), lens)]),
+                             dtype=np.uint8).copy()
+        data[100_000] ^= 0x01
+        engine_options(jl.OPT_LOG_HOST_THRESHOLD, jl.HOST_THRESHOLD_AUTO)
+        run = lambda: jl.log_verify(data)  # noqa: E731
+    outs, paths = [], []
+    for _ in range(40):
+        outs.append(run())
+        paths.append(jl.get_option(jl.INFO_LAST_PATH))
+        assert jl.get_option(jl.INFO_LAST_CALL_NS) > 0
+    assert all(np.array_equal(o, outs[0]) for o in outs)
+    assert paths[:4] == [1, 1, 0, 0], paths  # device twice, host twice
+    later = paths[4:]
+    assert 1 <= min(later.count(0), later.count(1)) <= 2, paths  # one path kept, the other re-measured
 
 
 def _table_file(oracle, rng, mib):

@@ -15,7 +15,7 @@ enough to run several rounds per wave with a partial last round.
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("log_path")]
 
 FUSED, TWO_PASS = 3, 2
 

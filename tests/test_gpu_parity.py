@@ -208,6 +208,7 @@ def _random_log(oracle, rng, n, max_len):
     return payloads, oracle.log_write(payloads)
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_golden(gpu, jl, oracle, golden):
     log = golden("log.bin")
     meta = golden("log.json")
@@ -217,6 +218,7 @@ def test_log_golden(gpu, jl, oracle, golden):
     assert (recs, reps) == oracle.log_read(log)
 
 
+@pytest.mark.usefixtures("log_path")
 @pytest.mark.parametrize("seed", range(6))
 def test_log_random_with_corruption(gpu, jl, oracle, seed):
     rng = np.random.default_rng(100 + seed)
@@ -234,6 +236,7 @@ def test_log_random_with_corruption(gpu, jl, oracle, seed):
         assert jl.log_read_records(log, True, initial) == oracle.log_read(log, True, initial)
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_special_records(gpu, jl, oracle):
     """Zero-type zero-length skip, bad length, stray trailer bytes, types 5..255."""
     base = oracle.log_write([b"a" * 100, b"b" * 10, b"c" * 20])
@@ -264,6 +267,7 @@ def test_log_special_records(gpu, jl, oracle):
             assert jl.log_read_records(log, checksum) == oracle.log_read(log, checksum)
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_corruption_recovery(gpu, jl, oracle):
     """TestCorruption.testRecovery (T/TestCorruption.java:250-270) through the device path."""
     from test_oracle import _batch_payload
@@ -291,6 +295,7 @@ def test_log_headers_dev(gpu, jl, oracle, golden):
     assert [bytes(h).hex() for h in hdr] == [c[2] for c in cases]
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_dev_resident(gpu, jl, oracle):
     rng = np.random.default_rng(9)
     payloads, log = _random_log(oracle, rng, 2000, 3000)
@@ -300,6 +305,7 @@ def test_log_dev_resident(gpu, jl, oracle):
     assert _events(got) == _events(oracle.log_events(log))
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_dev_async(gpu, jl, oracle):
     """jl_log_verify_dev_async: several logs verified back to back on one stream
     with no host round trip (a corrupted one, a tiny one, an empty one, and one of
@@ -329,7 +335,8 @@ def test_log_dev_async(gpu, jl, oracle):
     for log, d, ev, res in runs:
         n, n_dense, capf = (int(x) for x in res.cpu().numpy())
         assert capf == 0
-        assert (n_dense > 0) == (log is logs[-1])
+        if jl.get_option(jl.OPT_LOG_SMALL_MAX) == 0:  # the chunked path counts its dense blocks (lc_small: 0)
+            assert (n_dense > 0) == (log is logs[-1])
         got = np.frombuffer(ev.cpu().numpy().tobytes()[: n * 16], dtype=jl.LOG_EVENT_DTYPE)
         assert _events(got) == _events(oracle.log_events(log))
 
@@ -404,6 +411,7 @@ def test_log_emit_dev_matches_logwriter(gpu, jl, oracle, dest_length):
         assert reps == [] and [r[1] for r in recs] == payloads
 
 
+@pytest.mark.usefixtures("log_path")
 def test_log_many_small_records(gpu, jl, oracle):
     """Blocks with far more than 64 physical records (the walk keeps the first 64
     decisions of a block and re-walks the rest) next to blocks with fewer, with
