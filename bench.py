@@ -342,20 +342,31 @@ def dispatch_latency(oracle_free=True):
     """Per-call latency at the reference's call granularity (host memory, as an
     mmap'd file): one table of ~4.2 KB blocks (Options.java:206,208: 4 KiB blocks,
     2 MiB tables) and one WAL of 1 056-B records (Options.java:203: 4 MiB write
-    buffer), at several sizes, through the device path (JL_OPT_HOST_THRESHOLD 0)
-    and the host SSE4.2 path (threshold above the size).  Median of repeated calls;
-    the crossover is the smallest size from which the device is faster."""
+    buffer), at several sizes, through the device path (threshold 0), the host
+    SSE4.2 path (threshold above the size) and the engine's default, the auto
+    dispatch (JL_HOST_THRESHOLD_AUTO: both paths measured per size class, then
+    the faster one).  Medians of repeated calls; the crossover is the smallest
+    size from which the device is faster.  Per size also the device call's
+    staging-copy rate (pageable -> pinned, JL_INFO_LAST_STAGE_NS) and the share of
+    the auto calls that ran on the device; the copy pool's threads at the end."""
     rng = np.random.default_rng(SEED + 17)
     prev = (jl.get_option(jl.OPT_HOST_THRESHOLD), jl.get_option(jl.OPT_LOG_HOST_THRESHOLD))
 
-    def med(fn, reps):
+    def med(fn, reps, path_log=None):
         fn()
         ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
             fn()
             ts.append(time.perf_counter() - t0)
+            if path_log is not None:
+                path_log.append(jl.get_option(jl.INFO_LAST_PATH))
         return float(np.median(ts)) * 1e6
+
+    def stage_rate(fn, nbytes):
+        fn()
+        ns = jl.get_option(jl.INFO_LAST_STAGE_NS)
+        return round(nbytes / ns, 2) if ns > 0 else None  # GB/s
 
     res = {"table": [], "log": []}
     for mib in (0.25, 1, 2, 4, 8, 16, 64):
@@ -368,13 +379,22 @@ def dispatch_latency(oracle_free=True):
         src = torch.empty(int(lens.sum(dtype=np.uint64)), dtype=torch.uint8, device="cuda")
         jl.fill_random_dev(src, SEED + 19)
         log = jl.log_emit_dev(src, plan).cpu().numpy().copy()
-        reps = 30 if mib <= 4 else 8
+        reps = 30 if mib <= 4 else 12
         row_t, row_l = {"MiB": mib}, {"MiB": mib}
-        for path, thr in (("device_us", 0), ("host_us", 1 << 40)):
+        run_t = lambda: jl.table_verify(table, offs, sizes)  # noqa: E731
+        run_l = lambda: jl.log_verify(log)  # noqa: E731
+        for path, thr in (("device_us", 0), ("host_us", 1 << 40), ("auto_us", jl.HOST_THRESHOLD_AUTO)):
             jl.set_option(jl.OPT_HOST_THRESHOLD, thr)
             jl.set_option(jl.OPT_LOG_HOST_THRESHOLD, thr)
-            row_t[path] = round(med(lambda: jl.table_verify(table, offs, sizes), reps), 1)
-            row_l[path] = round(med(lambda: jl.log_verify(log), reps), 1)
+            pt, pl = [], []
+            row_t[path] = round(med(run_t, reps, pt), 1)
+            row_l[path] = round(med(run_l, reps, pl), 1)
+            if path == "device_us":
+                row_t["device_stage_GBps"] = stage_rate(run_t, table.size)
+                row_l["device_stage_GBps"] = stage_rate(run_l, log.size)
+            if path == "auto_us":
+                row_t["auto_device_share"] = round(pt.count(1) / len(pt), 2)
+                row_l["auto_device_share"] = round(pl.count(1) / len(pl), 2)
         res["table"].append(row_t)
         res["log"].append(row_l)
     jl.set_option(jl.OPT_HOST_THRESHOLD, prev[0])
@@ -382,9 +402,15 @@ def dispatch_latency(oracle_free=True):
     for k in ("table", "log"):
         faster = [r["MiB"] for r in res[k] if r["device_us"] < r["host_us"]]
         res[f"{k}_crossover_MiB"] = min(faster) if faster else None
-    res["config"] = ("per-call latency, host-memory input (pageable), device path vs the host SSE4.2 path: one table "
-                     "of ~4.2 KB blocks and one WAL of 1 056-B records per call, 1 calling thread")
+        # the default (auto) against the better of the two fixed paths, worst size
+        res[f"{k}_auto_vs_best"] = round(max(r["auto_us"] / min(r["device_us"], r["host_us"]) for r in res[k]), 3)
+    res["config"] = ("per-call latency, host-memory input (pageable), device path vs the host SSE4.2 path vs the "
+                     "default auto dispatch: one table of ~4.2 KB blocks and one WAL of 1 056-B records per call, "
+                     "1 calling thread")
     res["host_threshold_default_bytes"] = {"tables_batches": prev[0], "logs": prev[1]}
+    res["stage_pool"] = {"workers": jl.get_option(jl.INFO_STAGE_WORKERS),
+                         "spawn_failures": jl.get_option(jl.INFO_STAGE_SPAWN_FAILURES),
+                         "threads_option": jl.get_option(jl.OPT_STAGE_THREADS)}
     return res
 
 
@@ -420,6 +446,9 @@ def copy_inclusive_c2(data):
         t0 = time.perf_counter()
         got = jl.crc32c_fixed(pageable, 4096)
         res[key] = round(nbytes / (time.perf_counter() - t0) / GIB, 2)
+        if not reg:  # the host side of the staged leg: pageable -> pinned copies (the copy pool)
+            ns = jl.get_option(jl.INFO_LAST_STAGE_NS)
+            res["pageable_staged_copy_GBps"] = round(nbytes / ns, 2) if ns > 0 else None
         same = same and bool(np.array_equal(ref, got))
     jl.set_option(jl.OPT_HOST_REGISTER, prev)
     res["parity_with_device_resident"] = same

@@ -133,6 +133,13 @@ struct Workspace {
     // zeroed by the last kernel of each verification for the next one; a call that
     // stopped between its launches (or a new ws_lc) leaves them to a memset
     bool lc_dirty = true;
+    uint32_t lc_gen = 0;  // the last chunked verification's tag (lc_dwalk -> lc_dense readiness)
+    // lc_dwalk beside lc_dense (JL_OPT_DWALK_LANES > 0): its stream, the event it
+    // waits for (lc_walk done) and its own completion (waited for by the next
+    // verification of this workspace before lc_walk rewrites the dense list)
+    hipStream_t dw_st = nullptr;
+    hipEvent_t e_walk = nullptr, e_dw = nullptr;
+    bool dw_pending = false;
     hipStream_t async_st = nullptr;
     hipEvent_t async_done = nullptr;
     Slot slot[2];
@@ -140,6 +147,12 @@ struct Workspace {
         if (stream) (void)hipStreamSynchronize(stream);
         if (async_pending) (void)hipEventSynchronize(async_done);
         async_pending = false;
+        if (dw_st) (void)hipStreamSynchronize(dw_st);
+        for (hipEvent_t *e : {&e_walk, &e_dw})
+            if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+        if (dw_st) (void)hipStreamDestroy(dw_st);
+        dw_st = nullptr;
+        dw_pending = false;
         if (async_done) (void)hipEventDestroy(async_done);
         async_done = nullptr;
         if (h_res) (void)hipHostFree(h_res);
@@ -250,6 +263,7 @@ struct Options {
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
     int failpoint = 0;                // JL_OPT_FAILPOINT (tests): bit 0 perturbs lc_dwalk's offsets
     int64_t log_small_max = kLogSmallMaxDefault;  // JL_OPT_LOG_SMALL_MAX: logs up to this size verify in one launch
+    int64_t dwalk_lanes = 0;  // JL_OPT_DWALK_LANES: 0 = lc_dwalk before lc_dense; N = beside it, N lanes
 };
 Options &opt() {
     static Options o;
@@ -257,19 +271,26 @@ Options &opt() {
 }
 
 // ------------------------------------------------------------ call dispatch
-// Auto dispatch state: per kind of call (blocks: crc batches and tables; logs)
-// and size class (2^17 .. 2^28 bytes), the two paths' recent cost per byte.
-constexpr int kKindBlocks = 0, kKindLog = 1, kDispBuckets = 12, kDispExplore = 32;
-constexpr uint64_t kDispHostBelow = 128u << 10;    // auto: always the host below this
-constexpr uint64_t kDispDeviceFrom = 256ull << 20;  // auto: always the device from this
+// Auto dispatch state: per kind of call (the entry point) and size class (2^17 ..
+// 2^25 bytes), the two paths' cost per byte.  A class first alternates the paths
+// until each has kDispProbe calls (the median of those: a cold first call, page
+// faults of a fresh buffer, do not decide it), then every call takes the cheaper
+// path and feeds its average; the other path is measured again every 16 calls
+// when the two are within 25 %, every 64 within 2x, else every 256 (a box whose
+// costs drift, e.g. under host load, is followed; a clear loser costs < 1 %).
+constexpr int kKindFixed = 0, kKindBatch = 1, kKindTable = 2, kKindTables = 3, kKindLog = 4, kDispKinds = 5;
+constexpr int kDispBuckets = 9, kDispProbe = 3;
+constexpr uint64_t kDispHostBelow = 128u << 10;   // auto: always the host below this
+constexpr uint64_t kDispDeviceFrom = 64ull << 20;  // auto: always the device from this (host 3-4x slower)
 struct Dispatch {
     struct Cell {
         double ns_per_byte[2] = {0.0, 0.0};  // [0] host path, [1] device path
-        uint32_t n[2] = {0u, 0u};             // calls measured
-        uint32_t calls = 0;
+        double probe[2][kDispProbe] = {};
+        uint32_t n[2] = {0u, 0u};  // calls measured
+        uint32_t since = 0;        // calls since the other path was last measured
     };
     std::mutex mu;
-    Cell cell[2][kDispBuckets];
+    Cell cell[kDispKinds][kDispBuckets];
 };
 Dispatch &dispatch() {
     static Dispatch d;
@@ -297,10 +318,15 @@ struct Route {
             Dispatch &D = dispatch();
             std::lock_guard<std::mutex> lk(D.mu);
             Dispatch::Cell &c = D.cell[kind][bucket];
-            c.calls++;
-            if (c.n[1] < 2) host = false;       // measure the device path (the first call is a cold one)
-            else if (c.n[0] < 2) host = true;   // then the host path
-            else host = (c.ns_per_byte[0] <= c.ns_per_byte[1]) != (c.calls % kDispExplore == 0);
+            if (c.n[0] < kDispProbe || c.n[1] < kDispProbe) {
+                host = c.n[0] < c.n[1];  // alternate, the device first
+            } else {
+                const bool h = c.ns_per_byte[0] <= c.ns_per_byte[1];
+                const double r = h ? c.ns_per_byte[1] / c.ns_per_byte[0] : c.ns_per_byte[0] / c.ns_per_byte[1];
+                const uint32_t every = r < 1.25 ? 16u : (r < 2.0 ? 64u : 256u);
+                host = ++c.since >= every ? !h : h;
+                if (host != h) c.since = 0;
+            }
         }
         t_last_path = host ? 0 : 1;
     }
@@ -314,9 +340,15 @@ struct Route {
         Dispatch::Cell &c = D.cell[kind][bucket];
         const int p = host ? 0 : 1;
         const double v = (double)ns / (double)bytes;
-        // the first measurement of a path in a class is replaced by the second (first-use
-        // allocations, cold pages), later ones enter an average that follows drift
-        c.ns_per_byte[p] = c.n[p] < 2 ? v : 0.75 * c.ns_per_byte[p] + 0.25 * v;
+        if (c.n[p] < kDispProbe) {
+            c.probe[p][c.n[p]] = v;
+            if (c.n[p] + 1 == kDispProbe) {  // the median of the probe calls
+                double *q = c.probe[p];
+                c.ns_per_byte[p] = std::max(std::min(q[0], q[1]), std::min(std::max(q[0], q[1]), q[2]));
+            }
+        } else {
+            c.ns_per_byte[p] = 0.75 * c.ns_per_byte[p] + 0.25 * v;
+        }
         c.n[p]++;
     }
 };
@@ -858,6 +890,10 @@ int jl_set_option(int option, int64_t value) {
         if (value < 0 || value > (int64_t)JL_STREAM_CHUNK_BYTES) break;
         o.log_small_max = value;
         return JL_OK;
+    case JL_OPT_DWALK_LANES:
+        if (value < 0 || value > (1 << 24)) break;
+        o.dwalk_lanes = value;
+        return JL_OK;
     default:
         return fail(JL_ERR_INVALID, "jl_set_option: unknown option " + std::to_string(option));
     }
@@ -878,6 +914,7 @@ int64_t jl_get_option(int option) {
     case JL_OPT_STAGE_PIECE: return o.stage_piece;
     case JL_OPT_FAILPOINT: return o.failpoint;
     case JL_OPT_LOG_SMALL_MAX: return o.log_small_max;
+    case JL_OPT_DWALK_LANES: return o.dwalk_lanes;
     case JL_INFO_STAGE_WORKERS: return copy_pool().workers();
     case JL_INFO_STAGE_SPAWN_FAILURES: return copy_pool().spawn_failures();
     case JL_INFO_LAST_PATH: return t_last_path;
@@ -1002,7 +1039,7 @@ int jl_crc32c_fixed(const uint8_t *host, uint64_t block_bytes, uint64_t n_blocks
     if (n_blocks == 0) return JL_OK;
     if (!host || !out || block_bytes == 0) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: bad arguments");
     if (block_bytes > JL_STREAM_CHUNK_BYTES) return fail(JL_ERR_INVALID, "jl_crc32c_fixed: block larger than a chunk");
-    Route rt(kKindBlocks, n_blocks * block_bytes, opt().host_threshold);
+    Route rt(kKindFixed, n_blocks * block_bytes, opt().host_threshold);
     if (rt.host) {  // the host SSE4.2 path
         jlhost::fixed(host, block_bytes, n_blocks, flags, out);
         rt.ok = true;
@@ -1063,7 +1100,7 @@ int jl_crc32c_batch(const uint8_t *base, uint64_t base_bytes, const uint64_t *of
             return fail(JL_ERR_INVALID, "jl_crc32c_batch: block out of range");
         touched += len[i];
     }
-    Route rt(kKindBlocks, touched, opt().host_threshold);
+    Route rt(kKindBatch, touched, opt().host_threshold);
     if (rt.host) {  // the host SSE4.2 path
         jlhost::batch(base, off, len, init, suffix, n, flags, out);
         rt.ok = true;
@@ -1144,7 +1181,7 @@ int jl_table_verify(const uint8_t *file, uint64_t file_bytes, const uint64_t *of
             return fail(JL_ERR_INVALID, "jl_table_verify: truncated block read");  // TableFormat.java:203-206
         touched += (uint64_t)size[i] + 5;
     }
-    Route rt(kKindBlocks, touched, opt().host_threshold);
+    Route rt(kKindTable, touched, opt().host_threshold);
     if (rt.host) {  // the host SSE4.2 path (one table)
         jlhost::table_verify(file, off, size, n, status);
         rt.ok = true;
@@ -1208,7 +1245,7 @@ int jl_tables_verify(uint64_t n_tables, const uint8_t *const *files, const uint6
         }
     }
     if (n == 0) return JL_OK;
-    Route rt(kKindBlocks, touched, opt().host_threshold);
+    Route rt(kKindTables, touched, opt().host_threshold);
     if (rt.host) {
         for (uint64_t t = 0; t < n_tables; t++)
             jlhost::table_verify(files[t], off + first[t], size + first[t], first[t + 1] - first[t], status + first[t]);
@@ -1393,7 +1430,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
                  o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
-                 o_di = o_nl + al(nb * 4), o_dw = o_di + al(nb * 4), o_end = o_dw + al(nb * jlk::kDWMax * 2);
+                 o_di = o_nl + al(nb * 4), o_dr = o_di + al(nb * 4), o_dw = o_dr + al(nb * 4),
+                 o_end = o_dw + al(nb * jlk::kDWMax * 2);
     const size_t lc_cap = c.ws_lc.cap;
     JL_HIP(c.ws_lc.ensure(o_end));
     if (c.ws_lc.cap != lc_cap) c.lc_dirty = true;  // a new buffer: its counters are not zero
@@ -1438,6 +1476,10 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.dense_list = (uint32_t *)(ws + o_dl);
     A.nlong = (uint32_t *)(ws + o_nl);
     A.dw_info = (uint32_t *)(ws + o_di);
+    A.dw_ready = (uint32_t *)(ws + o_dr);
+    if (++c.lc_gen == 0) c.lc_gen = 1;
+    A.gen = c.lc_gen;
+    A.failpoint = (uint32_t)(opt().failpoint & 1);
     A.dw_off = (uint16_t *)(ws + o_dw);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
@@ -1453,15 +1495,30 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
     // (lc_finish zeroes them again at the end; r5 dropped the memset here: a
     // 4.4 us fill dispatch plus a ~6 us gap before it in every verification)
+    if (c.ws_lc.cap != lc_cap) JL_HIP(hipMemsetAsync(A.dw_ready, 0, nb * 4, st));  // no tag matches
     if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
     c.lc_dirty = true;  // until the last launch of this verification is enqueued
+    // the previous verification's lc_dwalk (beside its lc_dense) reads the dense list
+    if (c.dw_pending) JL_HIP(hipStreamWaitEvent(st, c.e_dw, 0));
     JL_HIP(jlk::launch_lc_walk(A, st));
     // the dense blocks' headers (lc_dwalk, one lane per block), then their crcs
     // (lc_dense).  r5 measured lc_dwalk of half the list on a second stream beside
     // lc_dense of the other half: random lengths 2.64 -> 2.47 ms, but every other
     // set 3-5 % slower (the cross-stream waits and the extra launches, ~40 us)
-    JL_HIP(jlk::launch_lc_dwalk(A, st));
-    if (opt().failpoint & 1) JL_HIP(jlk::launch_lc_failpoint(A, st));
+    const uint32_t lanes = (uint32_t)opt().dwalk_lanes;
+    A.dw_conc = lanes != 0;
+    if (lanes) {  // beside lc_dense: a second stream, started once lc_walk listed the dense blocks
+        if (!c.dw_st) JL_HIP(hipStreamCreateWithFlags(&c.dw_st, hipStreamNonBlocking));
+        if (!c.e_walk) JL_HIP(hipEventCreateWithFlags(&c.e_walk, hipEventDisableTiming));
+        if (!c.e_dw) JL_HIP(hipEventCreateWithFlags(&c.e_dw, hipEventDisableTiming));
+        JL_HIP(hipEventRecord(c.e_walk, st));
+        JL_HIP(hipStreamWaitEvent(c.dw_st, c.e_walk, 0));
+        JL_HIP(jlk::launch_lc_dwalk(A, lanes, c.dw_st));
+        JL_HIP(hipEventRecord(c.e_dw, c.dw_st));
+        c.dw_pending = true;
+    } else {
+        JL_HIP(jlk::launch_lc_dwalk(A, 0, st));
+    }
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:
@@ -1673,7 +1730,7 @@ static int log_verify_small_host(Workspace &w, const uint8_t *log, uint64_t log_
 // Host-memory log verification: chunks of JL_STREAM_CHUNK_BYTES (whole 32 KiB
 // blocks, so no record straddles a chunk and the final short block is the last
 // chunk's) through the double-buffered pipeline; each chunk's events are moved
-// to file offsets and copied out while the next chunk's bytes are in flight.
+// to file offsets and copied out while the following chunks' bytes are in flight.
 int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_event *events, uint64_t cap,
                   uint64_t *n_events) {
     if (int r = ensure_ready()) return r;
@@ -1708,8 +1765,10 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     HostSrc src(log, log_bytes);
     uint64_t total = 0;
     // A chunk's events leave by DMA into its slot's pinned h_out, and the host
-    // copies them into the caller's array while the next chunk runs (the copy
-    // pool).  r4 copied them with one hipMemcpyAsync into the caller's pageable
+    // copies them into the caller's array (the copy pool) one chunk later:
+    // log_verify_impl returns chunk i's count only once chunk i's kernels are
+    // done, so the copy of chunk i-1's events overlaps chunk i's rebase and D2H
+    // and chunk i+1's H2D, not chunk i+1's kernels.  r4 copied them with one hipMemcpyAsync into the caller's pageable
     // array, which the runtime stages and the host waits for: on the DBBench set
     // (0.5 GB of events per 4 GiB) the call ran at 38 GiB/s from pinned input.
     struct Out {

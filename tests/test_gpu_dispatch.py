@@ -89,9 +89,10 @@ def test_threshold_option(jl, gpu, engine_options):
 
 @pytest.mark.parametrize("kind", ["table", "log"])
 def test_auto_dispatch(gpu, jl, oracle, engine_options, kind):
-    """JL_HOST_THRESHOLD_AUTO: in a size class the first calls run twice on each
-    path (JL_INFO_LAST_PATH shows which), every call's output is the same, and
-    once both are measured the calls keep to one path but for one in 32."""
+    """JL_HOST_THRESHOLD_AUTO: in a size class the first calls alternate the paths
+    until each ran three times (JL_INFO_LAST_PATH shows which), every call's
+    output is the same, and then the calls keep to one path, the other measured
+    again every 16 / 64 / 256 calls."""
     rng = np.random.default_rng(SEED + 5)
     if kind == "table":
         data, offs, sizes = _table_file(oracle, rng, 1.5)
@@ -112,9 +113,9 @@ def test_auto_dispatch(gpu, jl, oracle, engine_options, kind):
         paths.append(jl.get_option(jl.INFO_LAST_PATH))
         assert jl.get_option(jl.INFO_LAST_CALL_NS) > 0
     assert all(np.array_equal(o, outs[0]) for o in outs)
-    assert paths[:4] == [1, 1, 0, 0], paths  # device twice, host twice
-    later = paths[4:]
-    assert 1 <= min(later.count(0), later.count(1)) <= 2, paths  # one path kept, the other re-measured
+    assert paths[:6] == [1, 0, 1, 0, 1, 0], paths  # alternating, the device first
+    later = paths[6:]
+    assert min(later.count(0), later.count(1)) <= 3, paths  # one path kept, the other re-measured
 
 
 def _table_file(oracle, rng, mib):

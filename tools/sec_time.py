@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Device-resident timings of the general-path configs without CPU legs:
 C3 (bench.secondary_c3) and the C5 sets (bench.secondary_c5).
-Usage: python tools/sec_time.py [steps] [which: all | c3 | c5 | dispatch | <C5 set name>[,<set>...]]"""
+Usage: [JL_OPTS="option=value,..."] python tools/sec_time.py [steps] [which: all | c3 | c5 | dispatch | <C5 set name>[,<set>...]]"""
 import json
 import os
 import sys
@@ -17,6 +17,9 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 which = sys.argv[2] if len(sys.argv) > 2 else "all"
 torch.cuda.set_device(0)
 jl.init(0)
+for kv in filter(None, os.environ.get("JL_OPTS", "").split(",")):  # engine options for A/Bs: "option=value,..."
+    k, v = kv.split("=")
+    jl.set_option(int(k), int(v))
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream()
 if which == "all" or "c3" in which.split(","):
