@@ -119,11 +119,6 @@ const char *jl_version(void);
  *                            verified in one launch, one workgroup per 32 KiB
  *                            block; larger ones take the chunked path (walk,
  *                            rounds).  0 = always the chunked path.  Default 16 MiB
- *   JL_OPT_DWALK_LANES       chunked log path: 0 = the dense blocks' header walk
- *                            (lc_dwalk) runs before lc_dense; N > 0 = beside it on
- *                            a second stream, N lanes walking the blocks in the
- *                            order lc_dense takes them (lc_dense takes a block's
- *                            offsets once published).  Same events either way
  *   JL_OPT_FAILPOINT         tests only: bit 0 perturbs the dense blocks' header
  *                            offsets between lc_dwalk and lc_dense (a different
  *                            inconsistency per block); results must not change
@@ -140,7 +135,6 @@ const char *jl_version(void);
 #define JL_OPT_STAGE_PIECE 9
 #define JL_OPT_FAILPOINT 10
 #define JL_OPT_LOG_SMALL_MAX 11
-#define JL_OPT_DWALK_LANES 12
 #define JL_HOST_THRESHOLD_AUTO (-1)
 /* Read-only (jl_get_option; jl_set_option refuses them): the staging copy pool
  * and the calling thread's last host-memory call, for diagnostics.

@@ -214,7 +214,6 @@ OPT_HOST_REGISTER, OPT_STAGE_THREADS, OPT_HOST_THRESHOLD, OPT_LOG_HOST_THRESHOLD
 OPT_STAGE_PIECE = 9
 OPT_FAILPOINT = 10  # tests only
 OPT_LOG_SMALL_MAX = 11
-OPT_DWALK_LANES = 12
 HOST_THRESHOLD_AUTO = -1
 INFO_STAGE_WORKERS, INFO_STAGE_SPAWN_FAILURES, INFO_LAST_PATH, INFO_LAST_CALL_NS, INFO_LAST_STAGE_NS = 201, 202, 203, 204, 205
 PATH_AUTO, PATH_STREAM, PATH_GV4 = 0, 1, 2

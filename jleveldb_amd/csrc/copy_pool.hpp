@@ -7,6 +7,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstddef>
+#include <cstdint>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -66,6 +67,10 @@ class CopyPool {
             queued_.fetch_sub(1);
         }
     }
+    // a caller about to run on the host (the SSE4.2 path) stops the idle workers'
+    // spinning: spinners share the caller's cores (SMT siblings) and slowed the
+    // host path right after a device call, which misled the auto dispatch's probes
+    void quiesce() { epoch_.fetch_add(1, std::memory_order_relaxed); }
     int workers() const { return live_.load(); }  // threads running
     int spawn_failures() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -104,7 +109,8 @@ class CopyPool {
             if (q_.empty() && !stop_) {  // spin a while (unlocked) before sleeping
                 lk.unlock();
                 const auto t0 = std::chrono::steady_clock::now();
-                while (queued_.load() == 0 &&
+                const uint64_t e = epoch_.load(std::memory_order_relaxed);
+                while (queued_.load() == 0 && epoch_.load(std::memory_order_relaxed) == e &&
                        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() < kSpinUs)
                     __builtin_ia32_pause();
                 lk.lock();
@@ -129,6 +135,7 @@ class CopyPool {
     std::condition_variable cv_, done_;
     std::deque<Job *> q_;
     std::atomic<int> queued_{0};  // jobs in q_ (read by spinning workers without the lock)
+    std::atomic<uint64_t> epoch_{0};  // quiesce() calls: a change ends the workers' spinning
     std::vector<std::thread> th_;
     bool stop_ = false;
     int failures_ = 0;                                // threads that could not start (guarded by mu_)

@@ -133,13 +133,6 @@ struct Workspace {
     // zeroed by the last kernel of each verification for the next one; a call that
     // stopped between its launches (or a new ws_lc) leaves them to a memset
     bool lc_dirty = true;
-    uint32_t lc_gen = 0;  // the last chunked verification's tag (lc_dwalk -> lc_dense readiness)
-    // lc_dwalk beside lc_dense (JL_OPT_DWALK_LANES > 0): its stream, the event it
-    // waits for (lc_walk done) and its own completion (waited for by the next
-    // verification of this workspace before lc_walk rewrites the dense list)
-    hipStream_t dw_st = nullptr;
-    hipEvent_t e_walk = nullptr, e_dw = nullptr;
-    bool dw_pending = false;
     hipStream_t async_st = nullptr;
     hipEvent_t async_done = nullptr;
     Slot slot[2];
@@ -147,12 +140,6 @@ struct Workspace {
         if (stream) (void)hipStreamSynchronize(stream);
         if (async_pending) (void)hipEventSynchronize(async_done);
         async_pending = false;
-        if (dw_st) (void)hipStreamSynchronize(dw_st);
-        for (hipEvent_t *e : {&e_walk, &e_dw})
-            if (*e) (void)hipEventDestroy(*e), *e = nullptr;
-        if (dw_st) (void)hipStreamDestroy(dw_st);
-        dw_st = nullptr;
-        dw_pending = false;
         if (async_done) (void)hipEventDestroy(async_done);
         async_done = nullptr;
         if (h_res) (void)hipHostFree(h_res);
@@ -263,7 +250,6 @@ struct Options {
     int64_t log_host_threshold = kLogHostThresholdDefault;  // JL_OPT_LOG_HOST_THRESHOLD: the same for jl_log_verify
     int failpoint = 0;                // JL_OPT_FAILPOINT (tests): bit 0 perturbs lc_dwalk's offsets
     int64_t log_small_max = kLogSmallMaxDefault;  // JL_OPT_LOG_SMALL_MAX: logs up to this size verify in one launch
-    int64_t dwalk_lanes = 0;  // JL_OPT_DWALK_LANES: 0 = lc_dwalk before lc_dense; N = beside it, N lanes
 };
 Options &opt() {
     static Options o;
@@ -302,6 +288,7 @@ thread_local int64_t t_last_ns = 0, t_stage_ns = 0;
 
 // The route of one host-memory call: its path (threshold >= 0: fixed; auto: the
 // measured costs), its time recorded for the auto dispatch once it succeeded.
+jlhost::CopyPool &copy_pool();
 struct Route {
     int kind, bucket = -1;
     uint64_t bytes;
@@ -329,6 +316,7 @@ struct Route {
             }
         }
         t_last_path = host ? 0 : 1;
+        if (host) copy_pool().quiesce();
     }
     ~Route() {
         const int64_t ns =
@@ -890,10 +878,6 @@ int jl_set_option(int option, int64_t value) {
         if (value < 0 || value > (int64_t)JL_STREAM_CHUNK_BYTES) break;
         o.log_small_max = value;
         return JL_OK;
-    case JL_OPT_DWALK_LANES:
-        if (value < 0 || value > (1 << 24)) break;
-        o.dwalk_lanes = value;
-        return JL_OK;
     default:
         return fail(JL_ERR_INVALID, "jl_set_option: unknown option " + std::to_string(option));
     }
@@ -914,7 +898,6 @@ int64_t jl_get_option(int option) {
     case JL_OPT_STAGE_PIECE: return o.stage_piece;
     case JL_OPT_FAILPOINT: return o.failpoint;
     case JL_OPT_LOG_SMALL_MAX: return o.log_small_max;
-    case JL_OPT_DWALK_LANES: return o.dwalk_lanes;
     case JL_INFO_STAGE_WORKERS: return copy_pool().workers();
     case JL_INFO_STAGE_SPAWN_FAILURES: return copy_pool().spawn_failures();
     case JL_INFO_LAST_PATH: return t_last_path;
@@ -1430,7 +1413,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
                  o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
-                 o_di = o_nl + al(nb * 4), o_dr = o_di + al(nb * 4), o_dw = o_dr + al(nb * 4),
+                 o_di = o_nl + al(nb * 4), o_dw = o_di + al(nb * 4),
                  o_end = o_dw + al(nb * jlk::kDWMax * 2);
     const size_t lc_cap = c.ws_lc.cap;
     JL_HIP(c.ws_lc.ensure(o_end));
@@ -1476,10 +1459,6 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.dense_list = (uint32_t *)(ws + o_dl);
     A.nlong = (uint32_t *)(ws + o_nl);
     A.dw_info = (uint32_t *)(ws + o_di);
-    A.dw_ready = (uint32_t *)(ws + o_dr);
-    if (++c.lc_gen == 0) c.lc_gen = 1;
-    A.gen = c.lc_gen;
-    A.failpoint = (uint32_t)(opt().failpoint & 1);
     A.dw_off = (uint16_t *)(ws + o_dw);
     A.stash = (uint64_t *)c.ws_stash.p;
     A.stash_cap = stash_cap;
@@ -1495,30 +1474,18 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
     // (lc_finish zeroes them again at the end; r5 dropped the memset here: a
     // 4.4 us fill dispatch plus a ~6 us gap before it in every verification)
-    if (c.ws_lc.cap != lc_cap) JL_HIP(hipMemsetAsync(A.dw_ready, 0, nb * 4, st));  // no tag matches
     if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
     c.lc_dirty = true;  // until the last launch of this verification is enqueued
-    // the previous verification's lc_dwalk (beside its lc_dense) reads the dense list
-    if (c.dw_pending) JL_HIP(hipStreamWaitEvent(st, c.e_dw, 0));
     JL_HIP(jlk::launch_lc_walk(A, st));
     // the dense blocks' headers (lc_dwalk, one lane per block), then their crcs
     // (lc_dense).  r5 measured lc_dwalk of half the list on a second stream beside
     // lc_dense of the other half: random lengths 2.64 -> 2.47 ms, but every other
     // set 3-5 % slower (the cross-stream waits and the extra launches, ~40 us)
-    const uint32_t lanes = (uint32_t)opt().dwalk_lanes;
-    A.dw_conc = lanes != 0;
-    if (lanes) {  // beside lc_dense: a second stream, started once lc_walk listed the dense blocks
-        if (!c.dw_st) JL_HIP(hipStreamCreateWithFlags(&c.dw_st, hipStreamNonBlocking));
-        if (!c.e_walk) JL_HIP(hipEventCreateWithFlags(&c.e_walk, hipEventDisableTiming));
-        if (!c.e_dw) JL_HIP(hipEventCreateWithFlags(&c.e_dw, hipEventDisableTiming));
-        JL_HIP(hipEventRecord(c.e_walk, st));
-        JL_HIP(hipStreamWaitEvent(c.dw_st, c.e_walk, 0));
-        JL_HIP(jlk::launch_lc_dwalk(A, lanes, c.dw_st));
-        JL_HIP(hipEventRecord(c.e_dw, c.dw_st));
-        c.dw_pending = true;
-    } else {
-        JL_HIP(jlk::launch_lc_dwalk(A, 0, st));
-    }
+    // (r6: lc_dwalk on a second stream beside lc_dense, publishing each block to it,
+    // ran the random set 3 % faster than its base but needed publication checks in
+    // lc_dense that cost every dense set 2-3 %: branch study-r6-dwalk-lanes)
+    JL_HIP(jlk::launch_lc_dwalk(A, st));
+    if (opt().failpoint & 1) JL_HIP(jlk::launch_lc_failpoint(A, st));
     JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:

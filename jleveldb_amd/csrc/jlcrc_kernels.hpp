@@ -181,14 +181,6 @@ struct LCArgs {
     // and dw_info[b] = offsets | (where lc_dense's own walk resumes) << 16
     uint16_t *dw_off;
     uint32_t *dw_info;
-    // dw_conc: lc_dwalk runs beside lc_dense on a second stream; dw_ready[b] == gen
-    // then says block b's dw_off / dw_info are this call's (lc_dwalk's release
-    // store).  A hint only: lc_dense checks every offset it takes against the
-    // block's bytes, so offsets of another call (or torn ones) are never trusted
-    uint32_t *dw_ready;
-    uint32_t gen;        // this verification's tag (never 0)
-    uint32_t dw_conc;
-    uint32_t failpoint;  // JL_OPT_FAILPOINT bit 0: lc_dwalk perturbs its results (tests)
 };
 // crc_gv4_kernel's round dealing state in its LDS image (general_v4.hip): dwords
 // [kGvBatchDword, +32) = 16 batch slots {base, tag | reads << 26}, [kGvDynDword,
@@ -202,9 +194,7 @@ hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
-// lanes 0: one lane per dense block (before lc_dense on its stream); else a
-// persistent grid of `lanes` lanes walking the list in order (beside lc_dense)
-hipError_t launch_lc_dwalk(const LCArgs &A, uint32_t lanes, hipStream_t st);
+hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
 // Small logs in one launch (lc_small_kernel, log_chunks.hip): one workgroup per
 // 32 KiB block (the blocks in ticket order) stages the block in LDS, walks it
 // (readPhysicalRecord's decisions), checks every OK record's crc there (one
@@ -235,6 +225,9 @@ hipError_t launch_lc_small(const LSmallArgs &A, hipStream_t st);
 // the work counters were not zero when lc_walk started (an earlier verification of
 // this workspace stopped before lc_finish)
 constexpr uint32_t kLCFlagCapacity = 1u, kLCFlagInconsistent = 2u, kLCFlagStale = 4u;
+// JL_OPT_FAILPOINT (tests): lc_dwalk's offsets of the listed dense blocks
+// perturbed before lc_dense reads them (each of lc_dense's consistency checks hit)
+hipError_t launch_lc_failpoint(const LCArgs &A, hipStream_t st);
 // lc_dwalk: header offsets kept per dense block; a run of kDWRun equal records
 // ends its walk (lc_dense's trips measure runs 257 records at a time)
 constexpr uint32_t kDWMax = 512;

@@ -760,28 +760,12 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // every line of its blocks at the HBM's random-line rate: a line prefetch 256 or
 // 512 B ahead of each lane's walk made it slower (r5p, random 0-200 B set 2.62 ->
 // 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2).
-// JL_OPT_FAILPOINT (tests only): lc_dwalk's results of the listed blocks it walked,
-// perturbed one way per list index mod 6, so that each consistency check of
-// lc_dense's first pass meets offsets that disagree with the block's bytes:
-// 0 an inner offset one byte off, 1 more offsets than kDWMax, 2 the resume position
-// one byte off, 3 the first offset not 0, 4 the last offset past the block, 5 none.
-__device__ __forceinline__ void dw_failpoint(const LCArgs &A, uint32_t i, uint64_t b) {
-    const uint32_t info = A.dw_info[b], n = info & 0xffffu;
-    uint16_t *o = A.dw_off + b * kDWMax;
-    switch (i % 6u) {
-    case 0: if (n >= 2u) o[n / 2u] = (uint16_t)(o[n / 2u] + 1u); break;
-    case 1: A.dw_info[b] = (info & 0xffff0000u) | (kDWMax + 1u); break;
-    case 2: A.dw_info[b] = info + (1u << 16); break;
-    case 3: if (n) o[0] = 7u; break;
-    case 4: if (n) o[n - 1u] = 32765u; break;
-    default: break;
-    }
-}
-
-// One dense block's walk (lc_dwalk): its OK records' header offsets from 0 until the
-// first record that is not OK, a run of kDWRun equal records or kDWMax offsets.
-__device__ __forceinline__ void dw_walk(const LCArgs &A, uint64_t b) {
-    const uint64_t bs = b * 32768u;
+__global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.dense_ctr[0]) return;
+    const uint32_t e = A.dense_list[i];
+    if (e & kDWUniform) return;  // lc_walk: a run, lc_dense walks it (and reads no dw_info)
+    const uint64_t b = e, bs = b * 32768u;
     const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
     const uint8_t *blk = A.log + bs;
     lc_v4 *out = (lc_v4 *)(A.dw_off + b * kDWMax);
@@ -820,25 +804,31 @@ __device__ __forceinline__ void dw_walk(const LCArgs &A, uint64_t b) {
     A.dw_info[b] = n | (p << 16);
 }
 
-// lc_dwalk: lanes walk the listed blocks in list order (the order lc_dense takes
-// them), lane i entries i, i + lanes, ..., and publish each block with dw_ready[b]
-// = gen (a release store: its offsets and info first).  Launched on a second
-// stream beside lc_dense (JL_OPT_DWALK_LANES) with fewer lanes than blocks,
-// the early blocks are ready early and lc_dense takes a block's offsets as soon as
-// they are: the walk (random 128-B lines at the HBM's line rate, ~0 VALU) overlaps
-// lc_dense's crc phases (VALU / LDS).  Launched before lc_dense on its own stream
-// (the r5 order), one lane per entry.
-__global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
-    const uint32_t nd = A.dense_ctr[0];
-    const uint32_t stride = gridDim.x * 256u;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nd; i += stride) {
-        const uint32_t e = A.dense_list[i];
-        if (e & kDWUniform) continue;  // lc_walk: a run, lc_dense walks it (and reads no dw_info)
-        const uint64_t b = e;
-        dw_walk(A, b);
-        if (A.failpoint) dw_failpoint(A, i, b);
-        if (A.dw_conc) __hip_atomic_store(&A.dw_ready[b], A.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+// JL_OPT_FAILPOINT (tests only): lc_dwalk's results of the listed blocks it walked,
+// perturbed one way per list index mod 6, so that each consistency check of
+// lc_dense's first pass meets offsets that disagree with the block's bytes:
+// 0 an inner offset one byte off, 1 more offsets than kDWMax, 2 the resume position
+// one byte off, 3 the first offset not 0, 4 the last offset past the block, 5 none.
+__global__ __launch_bounds__(256) void lc_failpoint_kernel(LCArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= A.dense_ctr[0]) return;
+    const uint32_t e = A.dense_list[i];
+    if (e & kDWUniform) return;
+    const uint64_t b = e;
+    const uint32_t info = A.dw_info[b], n = info & 0xffffu;
+    uint16_t *o = A.dw_off + b * kDWMax;
+    switch (i % 6u) {
+    case 0: if (n >= 2u) o[n / 2u] = (uint16_t)(o[n / 2u] + 1u); break;
+    case 1: A.dw_info[b] = (info & 0xffff0000u) | (kDWMax + 1u); break;
+    case 2: A.dw_info[b] = info + (1u << 16); break;
+    case 3: if (n) o[0] = 7u; break;
+    case 4: if (n) o[n - 1u] = 32765u; break;
+    default: break;
     }
+}
+hipError_t launch_lc_failpoint(const LCArgs &A, hipStream_t st) {
+    hipLaunchKernelGGL(lc_failpoint_kernel, dim3((A.n_blocks + 255u) / 256u), dim3(256), 0, st, A);
+    return hipGetLastError();
 }
 
 constexpr uint32_t kLDThreads = 256;
@@ -1019,13 +1009,14 @@ struct LDPre {
 // global access (vmcnt(0): gfx950 counts loads and stores together), which held
 // each block's walk until the next block's prefetch had landed (r3 shader-clock
 // phase counters: ~6 K of ~16 K clocks per block).
-// The walks' header reads (lc_dense, lc_small) from a 512-B window of the staged
+// lc_small's walk reads its headers from a 512-B window of the staged
 // block held in registers, lane i its bytes 8 i .. 8 i + 7 of the window: a
 // header inside the window costs three v_readlane (scalar results, no wait), a
-// window one LDS trip per ~5 records of random lengths.  r5 read every header
-// from LDS: one dependent trip per record, queued behind the crc lookups of the
-// CU's other workgroups.  q must be uniform; bytes past the staged block and its
-// zero pad are never used (a header ends at most 3 bytes into the pad).
+// window one LDS trip per ~5 records of random lengths (r6: the small random-length
+// log 117 -> 89 us).  r5 read every header from LDS: one dependent trip per record.
+// lc_dense keeps the r5 form: the window cost its DBBench set ~1 % (r6j).
+// q must be uniform; bytes past the staged block and its zero pad are never used
+// (a header ends at most 3 bytes into the pad).
 struct LDWin {
     uint32_t wb = 0x80000000u, wx = 0, wy = 0;  // the window's base (a multiple of 8), this lane's dwords
     __device__ __forceinline__ uint32_t at(const uint32_t *dat, uint32_t q, uint32_t lane) {  // == lds32u(dat, q)
@@ -1072,7 +1063,7 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 constexpr uint32_t kLDLongDw = 128;
 static_assert(kLDLongDw * 4u * kLCSlots >= 32768u, "a block holds fewer long records than slots");
 __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
+    __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
     __shared__ uint32_t nt[2 * kLDTabDwords];  // tables of z^4, z^8 (ld_map)
     __shared__ uint32_t t0[256];
     __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
@@ -1083,8 +1074,6 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
     __shared__ uint32_t doff[kDWMax / 2];  // lc_dwalk's header offsets of the block (u16 pairs)
     __shared__ uint32_t s_inc;            // lc_dwalk's offsets disagree with the staged bytes
-    __shared__ uint32_t s_nr[2];          // (block parity) a thread fetched the offsets before lc_dwalk published them
-    __shared__ uint32_t s_rdy;            // thread 0: they are published now (else the block is walked here)
     const uint32_t nd = uni(A.dense_ctr[0]);
     uint32_t *const ctr = &A.dense_ctr[1];  // list entries taken
     if (nd == 0) return;  // no dense block in the log
@@ -1127,32 +1116,12 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
     uint64_t bp = ~0ull;  // the previous block (its first_bad is written once its crc phase is done)
     LDPre pre;
     if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
-    // lc_dwalk's offsets and info word of the block, fetched with its bytes.  Beside
-    // lc_dwalk (A.dw_conc) only once it published them: a relaxed load of dw_ready
-    // (pok: this thread saw the call's tag), then relaxed agent-scope loads of the
-    // offsets (past the CU's cache).  No acquire: an agent-scope acquire invalidates
-    // the CU's vector cache and the XCD's L2 lines of other agents' writes, and one
-    // per thread per block doubled lc_dense's time (r6j, random set 2.5 -> 5.3 ms
-    // with lc_dwalk before it).  Offsets read early or torn fail the checks below.
+    // lc_dwalk's offsets and info word of the block, fetched with its bytes
     uint32_t pofs = 0, pinfo = 0;
-    bool pok = true;
-    auto fetch = [&](uint64_t bb) {
-        pofs = pinfo = 0;
-        if (!A.dw_conc) {  // lc_dwalk ran before this kernel on its stream
-            pofs = ((const uint32_t *)(A.dw_off + bb * kDWMax))[t];
-            pinfo = A.dw_info[bb];
-            return;
-        }
-        pok = __hip_atomic_load(&A.dw_ready[bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.gen;
-        if (pok) {
-            pofs = __hip_atomic_load((const uint32_t *)(A.dw_off + bb * kDWMax) + t, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-            pinfo = __hip_atomic_load(&A.dw_info[bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    };
-    if (b < A.n_blocks && !(be & kDWUniform)) fetch(b);
-    if (t < 2) s_nr[t] = 0;
-    uint32_t par = 0;  // uniform: block parity (s_nr)
+    if (b < A.n_blocks && !(be & kDWUniform)) {
+        pofs = ((const uint32_t *)(A.dw_off + b * kDWMax))[t];
+        pinfo = A.dw_info[b];
+    }
     unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
     uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
     while (b < A.n_blocks) {
@@ -1174,9 +1143,8 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         if (t < 4) dat[8192 + t] = 0;
         doff[t] = pofs;
-        if (!pok) atomicOr(&s_nr[par], 1u);
         if (t <= 32u) run_b[t] = 0;  // the sort's bucket counts (lc_dwalk's pass)
-        uint32_t dinfo = uni(pinfo);  // lc_dwalk: offsets | resume << 16 (0: none)
+        const uint32_t dinfo = uni(pinfo);  // lc_dwalk: offsets | resume << 16 (0: none)
         if (t == 0) {
             // the previous block's failure, read after the barrier above: its crc
             // phase ends with no barrier when it was the block's last pass, so a
@@ -1186,33 +1154,9 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             if (bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
             s_bad = kLCNone;
             s_inc = 0;
-            s_nr[par ^ 1u] = 0;  // the next block's (its last readers passed the barrier above)
         }
         bp = b;
         ld_sync();
-        if (uni(s_nr[par])) {
-            // lc_dwalk (beside this kernel on another stream) had not published the
-            // block when its offsets were fetched: thread 0 waits up to ~1 ms for it,
-            // then every thread fetches them again; past that the block is walked here
-            // (lc_dense's own walk from the block's start: the same events, slower)
-            if (t == 0) {
-                const uint64_t t0c = __builtin_amdgcn_s_memrealtime();
-                bool r = false;
-                while (!(r = __hip_atomic_load(&A.dw_ready[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.gen) &&
-                       __builtin_amdgcn_s_memrealtime() - t0c < 100000u)
-                    __builtin_amdgcn_s_sleep(8);
-                s_rdy = r;
-            }
-            ld_sync();
-            dinfo = 0;
-            if (uni(s_rdy)) {
-                fetch(b);
-                doff[t] = pofs;
-                dinfo = uni(pinfo);
-                ld_sync();
-            }
-        }
-        par ^= 1u;
         const uint64_t bne = sch.next(A, s_c[2], &moved), bn = bne & ~(uint64_t)kDWUniform;  // loads during this block
         if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
             grabbed = atomicAdd(ctr, sch.ch);
@@ -1220,8 +1164,10 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
         }
         if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
         pofs = pinfo = 0;
-        pok = true;
-        if (bn < A.n_blocks && !(bne & kDWUniform)) fetch(bn);
+        if (bn < A.n_blocks && !(bne & kDWUniform)) {
+            pofs = ((const uint32_t *)(A.dw_off + bn * kDWMax))[t];
+            pinfo = A.dw_info[bn];
+        }
         __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
         uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
         uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each; 0 once found inconsistent)
@@ -1248,7 +1194,6 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
             if (!ld_crc_ok(dat, T, h, len)) atomicMin(&s_bad, h);
         };
         auto doff16 = [&](uint32_t r) { return (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu; };
-        LDWin win;  // the walk's header reads
         while (!done) {
             // the block's failure so far: read before this pass's crc atomics can change it
             const bool crc = A.checksum && s_bad == kLCNone;
@@ -1325,7 +1270,7 @@ __global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
                 while (nr < kLDRuns) {
                     // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
                     // end); key = w >> 8 = length | type << 16
-                    const uint32_t rem = blen - p, w = win.at(dat, p + 3u, lane), key = w >> 8, len = key & 0xffffu;
+                    const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
                     if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
                         if (key == pk) {
                             // it repeats the record before it: the run is measured from here
@@ -1747,9 +1692,8 @@ uint32_t lc_dense_grid(int cus) {
     constexpr uint32_t lds = (8192 + 4) * 4 + 2 * kLDTabDwords * 4 + 256 * 4 + 2 * kLDRuns * 4 + kDWMax * 2 + 64;
     return (uint32_t)cus * (uint32_t)(kImageBytes / lds);
 }
-hipError_t launch_lc_dwalk(const LCArgs &A, uint32_t lanes, hipStream_t st) {
-    const uint32_t n = lanes ? (lanes < A.n_blocks ? lanes : A.n_blocks) : A.n_blocks;
-    hipLaunchKernelGGL(lc_dwalk_kernel, dim3((n + 255u) / 256u), dim3(256), 0, st, A);
+hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st) {
+    hipLaunchKernelGGL(lc_dwalk_kernel, dim3((A.n_blocks + 255u) / 256u), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {

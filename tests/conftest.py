@@ -58,15 +58,12 @@ def engine_options(jl):
         jl.set_option(option, value)
 
 
-@pytest.fixture(params=["small", "chunked", "chunked_dw"])
+@pytest.fixture(params=["small", "chunked"])
 def log_path(request, jl, engine_options):
-    """Runs a log test through the device paths: the one-launch small-log kernel
-    (lc_small, every log up to 64 MiB), the chunked path (walk, dense blocks,
-    rounds) forced for every size (JL_OPT_LOG_SMALL_MAX = 0), and the chunked
-    path with lc_dwalk running beside lc_dense on the second stream
-    (JL_OPT_DWALK_LANES)."""
+    """Runs a log test through both device paths: the one-launch small-log kernel
+    (lc_small, every log up to 64 MiB) and the chunked path (walk, dense blocks,
+    rounds) forced for every size (JL_OPT_LOG_SMALL_MAX = 0)."""
     engine_options(jl.OPT_LOG_SMALL_MAX, (64 << 20) if request.param == "small" else 0)
-    engine_options(jl.OPT_DWALK_LANES, 32768 if request.param == "chunked_dw" else 0)
     return request.param
 
 

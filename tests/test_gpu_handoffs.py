@@ -127,20 +127,15 @@ def test_long_and_short_failures_in_one_dense_block(gpu, jl, oracle):
     assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= len(cases)
 
 
-@pytest.mark.parametrize("lanes", [0, 32768])
 @pytest.mark.parametrize("maxlen", [40, 200, 800])
-def test_inconsistent_dwalk_offsets_recovered(gpu, jl, oracle, engine_options, maxlen, lanes):
+def test_inconsistent_dwalk_offsets_recovered(gpu, jl, oracle, maxlen):
     """lc_dense trusts lc_dwalk's header offsets only as the chain its staged
     bytes give (offsets that disagreed made it check garbage
     ranges and write long-record slots past the block's, an aperture fault in
     crc_gv4).  JL_OPT_FAILPOINT perturbs the offsets of every listed block five
     ways (an inner offset, the count past kDWMax, the resume position, the first
     offset, the last offset past the block); every such block must be re-walked
-    by lc_dense itself: events equal the oracle's, flips included, no fault.
-    Both lc_dwalk modes: before lc_dense on its stream (lanes 0) and beside it
-    on the second stream (JL_OPT_DWALK_LANES), where lc_dense reads a block's
-    offsets only after its ready flag carries the call's generation."""
-    engine_options(jl.OPT_DWALK_LANES, lanes)
+    by lc_dense itself: events equal the oracle's, flips included, no fault."""
     rng = np.random.default_rng(SEED + 7 * maxlen)
     lens = rng.integers(0, maxlen + 1, (48 << 20) // (maxlen // 2 + 7)).astype(np.uint32)
     log = _log(jl, gpu, lens)
