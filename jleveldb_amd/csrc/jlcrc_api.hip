@@ -227,9 +227,10 @@ int get_ws(Workspace **out) {
 // staged pageable input at a third of our sessions' rate (BENCH_r05: a 16 MiB
 // table 1 140 vs 505 us on the device, the same 1 180 vs 1 150 us on the host),
 // so no fixed size is right everywhere.  The default (JL_HOST_THRESHOLD_AUTO)
-// measures instead: per kind of call and size class the first calls run once or
-// twice on each path, then every call takes the faster one, and one call in 32
-// re-measures the other (Dispatch below).  A threshold >= 0 fixes the split.
+// measures instead: per entry point and size class the first calls alternate the
+// paths (three each, their median), then every call takes the faster one and the
+// other is re-measured every 16 / 64 / 256 calls (Dispatch below).  A threshold
+// >= 0 fixes the split.
 constexpr int64_t kHostThresholdDefault = JL_HOST_THRESHOLD_AUTO, kLogHostThresholdDefault = JL_HOST_THRESHOLD_AUTO;
 // Logs (and host-pipeline chunks of logs) up to this size take the one-launch path
 // (lc_small_kernel: one workgroup per 32 KiB block); larger ones the chunked path.
@@ -875,7 +876,7 @@ int jl_set_option(int option, int64_t value) {
         o.failpoint = (int)value;
         return JL_OK;
     case JL_OPT_LOG_SMALL_MAX:
-        if (value < 0 || value > (int64_t)JL_STREAM_CHUNK_BYTES) break;
+        if (value < 0 || value > (int64_t)1 << 40) break;  // host-memory logs: at most one chunk
         o.log_small_max = value;
         return JL_OK;
     default:
@@ -1716,7 +1717,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     if (int r = ws_order(*w, w->stream)) return r;
-    if (small_log(log_bytes, checksum)) {
+    if (small_log(log_bytes, checksum) && log_bytes <= JL_STREAM_CHUNK_BYTES) {
         const int rc = log_verify_small_host(*w, log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, events, cap, n_events);
         if (rc) (void)hipStreamSynchronize(w->stream);  // nothing of the call left in flight
         w->async_pending = false;  // w->stream waited for any earlier asynchronous call, and it is done

@@ -23,12 +23,11 @@ public final class Crc32CShims {
     static {
         int rc = Crc32CNative.init(0);
         if (rc != 0) throw new IllegalStateException("jlcrc: " + Crc32CNative.lastError());
-        // the call-size dispatch (DESIGN.md §1.3): a table or log smaller than the
-        // threshold is verified on the host's SSE4.2 path inside the engine; the
-        // defaults (the crossovers measured on fresh boxes, DESIGN.md §1.3: 4 MiB for
-        // tables, 16 MiB for logs) keep one 2 MiB table (maxFileSize) and one ~4 MiB
-        // WAL on the host and send a compaction's input tables (tablesVerify) and
-        // larger logs to the device
+        // the call-size dispatch (DESIGN.md §1.3): by default (JL_HOST_THRESHOLD_AUTO)
+        // the engine times both paths per entry point and size class on this box and
+        // sends each call to the faster one (below 128 KiB always the host's SSE4.2
+        // path, from 64 MiB always the device); a property fixes a threshold instead
+        // (a call smaller than it runs on the host)
         setThreshold(Crc32CNative.OPT_HOST_THRESHOLD, "jlcrc.hostThreshold");
         setThreshold(Crc32CNative.OPT_LOG_HOST_THRESHOLD, "jlcrc.logHostThreshold");
     }
