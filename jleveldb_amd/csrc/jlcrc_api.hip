@@ -133,6 +133,8 @@ struct Workspace {
     // zeroed by the last kernel of each verification for the next one; a call that
     // stopped between its launches (or a new ws_lc) leaves them to a memset
     bool lc_dirty = true;
+    uint32_t lc_gen = 0;  // the last chunked verification's tag (lc_dense's placement tiles)
+    uint32_t *h_hint = nullptr;  // pinned: the last chunked verification's count of lc_dwalk's blocks
     hipStream_t async_st = nullptr;
     hipEvent_t async_done = nullptr;
     Slot slot[2];
@@ -144,6 +146,8 @@ struct Workspace {
         async_done = nullptr;
         if (h_res) (void)hipHostFree(h_res);
         h_res = nullptr;
+        if (h_hint) (void)hipHostFree(h_hint);
+        h_hint = nullptr;
         for (DevBuf *b : {&ws_lc, &ws_slot, &ws_desc, &ws_big, &ws_part, &ws_tmp, &ws_stash, &ws_ls, &ws_lsev, &ws_small})
             b->release();
         small_dirty = true;
@@ -1412,7 +1416,8 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     const size_t hn = jlk::kLCCounters * ng + 1;
     const size_t o_cnt = 256, o_start = o_cnt + al((nb + 1) * 4), o_hist = o_start + al((nb + 1) * 8), o_hscan = o_hist + al(hn * 4),
                  o_rt = o_hscan + al(hn * 4), o_ts = o_rt + al(jlk::kLCCounters * 4),
-                 o_rs = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
+                 o_ts0 = o_ts + al((nb / jlk::kLSTile + 1) * 8), o_pr = o_ts0 + al((nb / jlk::kLSTile + 1) * 8),
+                 o_s0 = o_pr + al(nb * 4), o_rd = o_s0 + al((nb + 1) * 8), o_rs = o_rd + al((nb / jlk::kLSTile + 1) * 4), o_fb = o_rs + al((jlk::kLCBins + 1) * 4), o_do = o_fb + al(nb * 4),
                  o_flag = o_do + al(nb * 8), o_res = o_flag + 256, o_dl = o_res + 256, o_nl = o_dl + al(nb * 4),
                  o_di = o_nl + al(nb * 4), o_dw = o_di + al(nb * 4),
                  o_end = o_dw + al(nb * jlk::kDWMax * 2);
@@ -1451,12 +1456,19 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.hscan = (uint32_t *)(ws + o_hscan);
     A.rowtot = (uint32_t *)(ws + o_rt);
     A.tstat = (uint64_t *)(ws + o_ts);
+    A.tstat0 = (uint64_t *)(ws + o_ts0);
+    A.pred = (uint32_t *)(ws + o_pr);
+    A.start0 = (uint64_t *)(ws + o_s0);
+    A.ready0 = (uint32_t *)(ws + o_rd);
+    if (++c.lc_gen == 0) c.lc_gen = 1;
+    A.gen = c.lc_gen;
     A.rstart = (uint32_t *)(ws + o_rs);
     A.first_bad = (uint32_t *)(ws + o_fb);
     A.dense_off = (uint64_t *)(ws + o_do);
     A.cap_flag = (uint32_t *)(ws + o_flag);
     A.stash_ctr = (unsigned long long *)(ws + o_flag + 8);
     A.dense_ctr = (uint32_t *)ws;  // at a fixed place: the previous verification zeroed it
+    A.nu_ctr = A.dense_ctr + 6;
     A.dense_list = (uint32_t *)(ws + o_dl);
     A.nlong = (uint32_t *)(ws + o_nl);
     A.dw_info = (uint32_t *)(ws + o_di);
@@ -1472,10 +1484,11 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     A.seed0 = jlmath::slice4_inv(0xffffffffu);
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
-    // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids
+    // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids,
+    // [6] lc_dwalk's blocks
     // (lc_finish zeroes them again at the end; r5 dropped the memset here: a
     // 4.4 us fill dispatch plus a ~6 us gap before it in every verification)
-    if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 16, st));
+    if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 32, st));
     c.lc_dirty = true;  // until the last launch of this verification is enqueued
     JL_HIP(jlk::launch_lc_walk(A, st));
     // the dense blocks' headers (lc_dwalk, one lane per block), then their crcs
@@ -1487,7 +1500,14 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // lc_dense that cost every dense set 2-3 %: branch study-r6-dwalk-lanes)
     JL_HIP(jlk::launch_lc_dwalk(A, st));
     if (opt().failpoint & 1) JL_HIP(jlk::launch_lc_failpoint(A, st));
-    JL_HIP(jlk::launch_lc_dense(A, ctx().cus, st));
+    // the in-place kernel when the workspace's last verification had lc_dwalk's blocks
+    // (a log verified again, or the next chunk of one: a guess, either kernel is right)
+    if (!c.h_hint) {
+        JL_HIP(hipHostMalloc((void **)&c.h_hint, 64, hipHostMallocCoherent));
+        *c.h_hint = 0;
+    }
+    A.hint = c.h_hint;
+    JL_HIP(jlk::launch_lc_dense(A, ctx().cus, *(volatile uint32_t *)c.h_hint != 0u, st));
     JL_HIP(jlk::launch_lc_scan(A, st));  // event starts per block; chunk ranks per (bin, group)
     // capacities of the round table, the multi-chunk records and their chunk states:
     // <= kLCSlots records in a block that is not dense, and a block's bytes bound its extra chunks

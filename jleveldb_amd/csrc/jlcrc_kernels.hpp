@@ -124,7 +124,7 @@ constexpr uint32_t kLCCounters = kLCBins + 3;  // per group: bins, multi-chunk r
 // its exact event count and stashes its events (lc_build places them)
 constexpr uint32_t kLCSlots = 64;
 constexpr uint32_t kLCProbe = 4;
-constexpr uint32_t kLCDense = 0xffffffffu;  // count[b] of a dense block until lc_dense counts it
+constexpr uint32_t kLCDense = 0xffffffffu;  // count[b] of a dense block whose events were not predicted, until lc_dense counts it
 constexpr uint32_t kLDMaxEv = 4688;         // >= events (and runs) of one 32 KiB block (one per 7 bytes)
 constexpr uint32_t kLCNone = 0xffffffffu;  // first_bad: no failure
 struct LCBig {        // a record of more than one chunk
@@ -166,6 +166,17 @@ struct LCArgs {
     uint32_t seed0;        // slice4^-1(0xffffffff): value()'s seed as 4 bytes before a crc range
     uint32_t *dense_list;  // n_blocks: the dense blocks (lc_walk appends, lc_dense takes them in chunks)
     uint32_t *dense_ctr;   // [0] dense blocks listed, [1] list entries taken, [2] gv4 deal, [3] lc_scan ids (zero at the start; lc_finish re-zeroes them)
+    uint32_t *nu_ctr;      // dense_ctr + 6: lc_dwalk's blocks (lc_walk counts them; lc_finish zeroes it)
+    // in-place events of lc_dwalk's blocks (r6): every dense block's predicted event
+    // count (lc_walk / lc_dwalk; count[b] until lc_dense counts), the starts they give
+    // (lc_dense's first workgroups, by agent-scope atomics), its look-back statuses,
+    // and per tile of kLSTile blocks the call's tag once its starts are out
+    uint32_t *pred;
+    uint64_t *start0;
+    uint64_t *tstat0;
+    uint32_t *ready0;
+    uint32_t gen;    // this verification's tag (never 0)
+    uint32_t *hint;  // host-visible: lc_finish leaves *nu_ctr there (which lc_dense kernel comes next)
     uint32_t *cap_flag;    // set when a capacity was exceeded
     uint64_t *result;      // [0] events, [1] dense blocks, [2] cap_flag (written last)
     GDesc *desc;           // rounds * 8
@@ -193,7 +204,8 @@ hipError_t launch_lc_setup(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_build(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_combine(const LCArgs &A, hipStream_t st);
 hipError_t launch_lc_apply(const LCArgs &A, hipStream_t st);
-hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st);
+// inplace: lc_dense_inplace_kernel (lc_dwalk's blocks' events in place), else lc_dense_kernel
+hipError_t launch_lc_dense(const LCArgs &A, int cus, bool inplace, hipStream_t st);
 hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st);
 // Small logs in one launch (lc_small_kernel, log_chunks.hip): one workgroup per
 // 32 KiB block (the blocks in ticket order) stages the block in LDS, walks it
@@ -240,6 +252,7 @@ uint32_t lc_dense_grid(int cus);                  // lc_dense's workgroups
 constexpr uint64_t kLDPool = 16384;               // stash_pool of large logs
 constexpr uint32_t kLDRuns = 256;                 // runs per lc_dense pass (a stash segment: + 1 link)
 constexpr uint64_t kLCNotDense = 0xfffffffffffffffeull;
+constexpr uint64_t kLDPlaced = 1ull << 47;  // dense_off: lc_dense wrote the block's events in place
 #ifndef JL_LS_TILE
 #define JL_LS_TILE 4096  // study builds: 256 runs the multi-tile / multi-step paths on small logs
 #endif

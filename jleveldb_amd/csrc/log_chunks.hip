@@ -191,7 +191,10 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     uint32_t cnt = 0;
     bool listed = false;   // a dense block: appended to lc_dense's list below
     bool uniform = false;  // ... whose last walked records are equal (kDWUniform in its list entry)
-    if (b < (A.n_blocks + kLSTile) / kLSTile) A.tstat[b] = 0;  // lc_scan's look-back statuses
+    if (b < (A.n_blocks + kLSTile) / kLSTile) {  // the scans' look-back statuses, the placement's tile tags
+        A.tstat[b] = A.tstat0[b] = 0;
+        A.ready0[b] = 0;
+    }
     if (b < A.n_blocks) {
         if (A.checksum) A.first_bad[b] = kLCNone;
         A.nlong[b] = 0;  // lc_dense's deferred long records
@@ -246,7 +249,18 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
                 uniform = (uint32_t)sj == (uint32_t)s0;
             }
             uniform = uniform && (((uint32_t)s0 >> 24) & 0xffu) == 1u;
-            cnt = kLCDense;
+            // the block's events, predicted (lc_dwalk predicts the others): the run to
+            // the block's end, then the record that fills it (the writer's FIRST
+            // fragment, J/db/LogWriter.java:100-118) or the trailer.  lc_dwalk checks two
+            // headers of it when it matters (in-place events, lc_dense)
+            if (uniform) {
+                const uint32_t L = 7u + ((uint32_t)s0 & 0xffffu), left = (uint32_t)(be - p), rem = left % L;
+                cnt += left / L + (rem >= 7u || (eof && rem > 0u) ? 1u : 0u);
+                A.dw_info[b] = (uint32_t)(p - bs) | (L << 16);  // (lc_dense reads no dw_info of a run block)
+            } else {
+                cnt = kLCDense;
+            }
+            A.pred[b] = cnt;
             listed = true;
         }
         A.count[b] = cnt;
@@ -254,16 +268,19 @@ __global__ __launch_bounds__(256) void lc_walk_kernel(LCArgs A) {
     // the dense blocks into lc_dense's list: the waves' counts summed in LDS, one
     // global atomic per workgroup that has any (one per wave cost the DBBench set's
     // walk ~20 us: 2 048 atomics on one address at the same moment)
-    __shared__ uint32_t s_dn, s_db;
-    if (threadIdx.x == 0) s_dn = 0;
+    __shared__ uint32_t s_dn, s_db, s_nu;
+    if (threadIdx.x == 0) s_dn = s_nu = 0;
     __syncthreads();
     const uint64_t dm = __builtin_amdgcn_ballot_w64(listed);
+    const uint64_t nm = __builtin_amdgcn_ballot_w64(listed && !uniform);  // lc_dwalk's blocks
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t woff = 0;
     if (dm && lane == 0) woff = atomicAdd(&s_dn, (uint32_t)__builtin_popcountll(dm));
+    if (nm && lane == 0) atomicAdd(&s_nu, (uint32_t)__builtin_popcountll(nm));
     woff = (uint32_t)__builtin_amdgcn_readfirstlane((int)woff);
     __syncthreads();
     if (threadIdx.x == 0 && s_dn) s_db = atomicAdd(&A.dense_ctr[0], s_dn);
+    if (threadIdx.x == 0 && s_nu) atomicAdd(A.nu_ctr, s_nu);
     __syncthreads();
     if (listed)
         A.dense_list[s_db + woff + (uint32_t)__builtin_popcountll(dm & ((1ull << lane) - 1ull))] =
@@ -316,6 +333,62 @@ __device__ __forceinline__ uint32_t ls_block_excl(uint32_t v, uint32_t *wsum, ui
 }
 constexpr uint32_t kLSPer = kLSTile / 256u;  // values per thread
 static_assert(kLSTile % 256u == 0u, "kLSTile: a multiple of the workgroup");
+// One tile of kLSTile event starts (lc_scan; and lc_dwalk's first placement over
+// the predicted counts, r6): out[i] = the events of blocks [0, i), decoupled
+// look-back over the tiles' statuses (tstat, zeroed by lc_walk).
+// ready non-null (lc_dense's placement, read by other workgroups of the same
+// kernel): out[] by agent-scope atomic stores, then ready[id] = A.gen.
+__device__ __forceinline__ void ls_tile(const LCArgs &A, uint32_t id, uint64_t *tstat, uint64_t *out, uint32_t *buf,
+                                        uint32_t *wsum, unsigned long long *s_pre, uint32_t *ready = nullptr) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t k = id, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
+    for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
+    __syncthreads();
+    uint32_t v[kLSPer], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kLSPer; j++) {
+        v[j] = buf[kLSPer * t + j];
+        s += v[j];
+    }
+    uint32_t agg;
+    const uint32_t ex = ls_block_excl(s, wsum, &agg);
+    if (t == 0) {
+        uint64_t P = 0;
+        if (k == 0) {
+            __hip_atomic_store(&tstat[0], kLDInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&tstat[k], kLDAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t q = (int64_t)k - 1; q >= 0; q--) {
+                uint64_t w;
+                while ((w = __hip_atomic_load(&tstat[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
+                    __builtin_amdgcn_s_sleep(1);
+                P += w & kLDVal;
+                if (w & kLDInc) break;
+            }
+            __hip_atomic_store(&tstat[k], kLDInc | (P + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *s_pre = P;
+    }
+    __syncthreads();
+    const uint64_t pre = *s_pre;
+    uint32_t run = ex;
+#pragma unroll
+    for (uint32_t j = 0; j < kLSPer; j++) {  // exclusive values back into LDS, in place
+        buf[kLSPer * t + j] = run;
+        run += v[j];
+    }
+    __syncthreads();
+    for (uint32_t j = t; j < kLSTile; j += 256u) {
+        if (base + j >= n) continue;
+        if (ready) __hip_atomic_store(&out[base + j], pre + buf[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else out[base + j] = pre + buf[j];
+    }
+    if (ready) {
+        __syncthreads();  // every thread's stores done
+        if (t == 0) __hip_atomic_store(&ready[id], A.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Work ids come from a counter in dispatch order (dense_ctr[3], zero when
 // lc_walk starts), not from blockIdx.x: tile k's look-back spins on tiles k - 1 ..., so
 // it must not run before they have started, which a blockIdx order would only
@@ -335,45 +408,7 @@ __global__ __launch_bounds__(256) void lc_scan_kernel(LCArgs A) {
     }
     const uint32_t id = blockIdx.x >= kLCCounters ? s_id : tiles + blockIdx.x;
     if (id < tiles) {
-        const uint64_t k = id, base = k * kLSTile, n = (uint64_t)A.n_blocks + 1u;
-        for (uint32_t j = t; j < kLSTile; j += 256u) buf[j] = base + j < n ? A.count[base + j] : 0u;
-        __syncthreads();
-        uint32_t v[kLSPer], s = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kLSPer; j++) {
-            v[j] = buf[kLSPer * t + j];
-            s += v[j];
-        }
-        uint32_t agg;
-        const uint32_t ex = ls_block_excl(s, wsum, &agg);
-        if (t == 0) {
-            uint64_t P = 0;
-            if (k == 0) {
-                __hip_atomic_store(&A.tstat[0], kLDInc | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                __hip_atomic_store(&A.tstat[k], kLDAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (int64_t q = (int64_t)k - 1; q >= 0; q--) {
-                    uint64_t w;
-                    while ((w = __hip_atomic_load(&A.tstat[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0)
-                        __builtin_amdgcn_s_sleep(1);
-                    P += w & kLDVal;
-                    if (w & kLDInc) break;
-                }
-                __hip_atomic_store(&A.tstat[k], kLDInc | (P + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            s_pre = P;
-        }
-        __syncthreads();
-        const uint64_t pre = s_pre;
-        uint32_t run = ex;
-#pragma unroll
-        for (uint32_t j = 0; j < kLSPer; j++) {  // exclusive values back into LDS, in place
-            buf[kLSPer * t + j] = run;
-            run += v[j];
-        }
-        __syncthreads();
-        for (uint32_t j = t; j < kLSTile; j += 256u)
-            if (base + j < n) A.start[base + j] = pre + buf[j];
+        ls_tile(A, id, A.tstat, A.start, buf, wsum, &s_pre);
         return;
     }
     const uint32_t c = id - tiles;  // a hist row
@@ -600,6 +635,8 @@ __device__ __forceinline__ void lc_finish(const LCArgs &A) {
         A.result[1] = A.rowtot[kLCOver];
         A.result[2] = *A.cap_flag;
         lc_st16(A.dense_ctr, lc_v4{0u, 0u, 0u, 0u});
+        if (A.hint) *A.hint = *A.nu_ctr;  // the host's guess for the next verification's lc_dense
+        lc_st16(A.dense_ctr + 4, lc_v4{0u, 0u, 0u, 0u});  // [6] nu_ctr
     }
 }
 
@@ -625,6 +662,15 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
         nl[i] = b < A.n_blocks ? A.nlong[b] : 0u;   // dense blocks: long records left to the rounds
         st[i] = b < A.n_blocks ? A.start[b] : 0u;
         doff[i] = b < A.n_blocks ? A.dense_off[b] : kLCNotDense;
+    }
+    // a block whose events lc_dense wrote in place keeps them where its count was
+    // as predicted and its start as placed then; else its stashed runs are expanded
+    // here as any dense block's (a wrong prediction moves the blocks after it)
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++) {
+        const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
+        if (doff[i] != kLCNotDense && doff[i] != ~0ull && (doff[i] & kLDPlaced))
+            doff[i] = cnt[i] == A.pred[b] && st[i] == A.start0[b] ? ~0ull : doff[i] & ~kLDPlaced;
     }
     // a block's walk slots, or a dense block's first 64 stash entries (its runs)
 #pragma unroll
@@ -760,13 +806,30 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // every line of its blocks at the HBM's random-line rate: a line prefetch 256 or
 // 512 B ahead of each lane's walk made it slower (r5p, random 0-200 B set 2.62 ->
 // 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2).
-__global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= A.dense_ctr[0]) return;
+// One listed dense block (lc_dwalk's lane): a run block's prediction checked, the
+// others' headers walked and their events predicted (count[b] = pred[b]).
+__device__ __forceinline__ void dw_block(const LCArgs &A, uint32_t i) {
     const uint32_t e = A.dense_list[i];
-    if (e & kDWUniform) return;  // lc_walk: a run, lc_dense walks it (and reads no dw_info)
-    const uint64_t b = e, bs = b * 32768u;
+    const uint64_t b = e & ~kDWUniform, bs = b * 32768u;
     const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+    if (e & kDWUniform) {
+        // lc_walk: a run, lc_dense walks it.  Its predicted event count (lc_walk's,
+        // from the walked records) places the blocks after it, which matters only
+        // when lc_dense writes events in place (some dense block is lc_dwalk's):
+        // checked at two headers, the next one repeats the run's length and the one
+        // after the run's predicted end fills the block.  A block of records of
+        // random lengths whose last walked ones were equal by chance fails and is
+        // walked here instead (a wrong prediction costs lc_build the blocks after it)
+        if (*A.nu_ctr == 0u) return;
+        const uint32_t info = A.dw_info[b], p = info & 0xffffu, L = info >> 16, left = blen - p;
+        const uint32_t rem = left % L, k = left / L;
+        const uint64_t h1 = k ? lc_header(A.log + bs + p, left) : 0ull;
+        const uint64_t h2 = rem >= 7u ? lc_header(A.log + bs + p + k * L, rem) : 0ull;
+        const bool ok1 = !k || 7u + ((uint32_t)(h1 >> 32) & 0xffffu) == L;
+        const bool ok2 = rem < 7u || 7u + ((uint32_t)(h2 >> 32) & 0xffffu) == rem;
+        if (ok1 && ok2) return;
+        A.dense_list[i] = (uint32_t)b;  // not a run after all: walked here, its offsets to lc_dense
+    }
     const uint8_t *blk = A.log + bs;
     lc_v4 *out = (lc_v4 *)(A.dw_off + b * kDWMax);
     uint32_t p = 0, n = 0, pk = ~0u, eq = 0;
@@ -802,6 +865,25 @@ __global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
         if (n > n0) out[n0 / 8u] = lc_v4{q[0], q[1], q[2], q[3]};
     }
     A.dw_info[b] = n | (p << 16);
+    // the block's events when the walk ended at its end (then the trailer, or the
+    // file's short last block's kind-6 event) or at a record that is not OK (its
+    // event ends lc_dense's walk); after a run or kDWMax offsets: not predicted
+    // (kLCDense: the placement of the blocks after it is lc_build's)
+    const uint32_t rem = blen - p;
+    uint32_t pred = kLCDense;
+    if (rem < 7u) {
+        pred = n + (blen < 32768u && rem > 0u ? 1u : 0u);
+    } else if (n < kDWMax) {
+        const uint32_t key = (uint32_t)(lc_header(blk + p, rem) >> 32) & 0xffffffu;
+        if (rem < 7u + (key & 0xffffu) || key == 0u) pred = n + 1u;
+    }
+    A.count[b] = A.pred[b] = pred;
+}
+
+// lc_dwalk: one lane per listed dense block (dw_block)
+__global__ __launch_bounds__(256) void lc_dwalk_kernel(LCArgs A) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < A.dense_ctr[0]) dw_block(A, i);
 }
 
 // JL_OPT_FAILPOINT (tests only): lc_dwalk's results of the listed blocks it walked,
@@ -1060,341 +1142,64 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 // left in the block's walk slots (nlong[b] of them) for lc_build to place, the
 // crc checked by crc_gv4_kernel<MODE_LOG_CHUNK> / lc_combine, a failure
 // atomicMin'ed into first_bad[b] like the block's own.
+// lc_dense's in-place events (lc_dwalk's blocks; only lc_dense_kernel<true>).
+// The block's first event's place (lc_dense's first workgroups' placement, once
+// its tile is out).
+__device__ __forceinline__ uint64_t ld_start0(const LCArgs &A, uint64_t b) {
+    while (__hip_atomic_load(&A.ready0[b / kLSTile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.gen)
+        __builtin_amdgcn_s_sleep(2);
+    return uni64(__hip_atomic_load(&A.start0[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// events [ev0, ev0 + m) of block b: lc_dwalk's records, one each (header offsets doff)
+__device__ __forceinline__ void ld_place_dw(const LCArgs &A, const uint32_t *dat, const uint32_t *doff, uint64_t b,
+                                         uint32_t ev0, uint32_t m) {
+    const uint64_t st0 = ld_start0(A, b) + ev0;
+    for (uint32_t r = threadIdx.x; r < m; r += 256u) {
+        const uint32_t h = (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu;
+        const uint32_t w = __builtin_amdgcn_alignbyte(dat[((h + 3u) >> 2) + 1u], dat[(h + 3u) >> 2], (h + 3u) & 3u);
+        lc_event(A, st0 + r, b * 32768u + h, (w >> 8) & 0xffffu, w >> 24, 1u);
+    }
+}
+// events [ev0, ev0 + nev) of block b from a walk pass's runs
+__device__ __forceinline__ void ld_place_runs(const LCArgs &A, const uint32_t *run_a, const uint32_t *run_b, uint64_t b,
+                                           uint32_t ev0, uint32_t nr, uint32_t nev) {
+    const uint64_t st0 = ld_start0(A, b) + ev0;
+    for (uint32_t r = threadIdx.x; r < nev; r += 256u) {
+        uint32_t j = 0;  // the run holding event r (as in the crc phase)
+        for (uint32_t sh = nr > 1u ? 1u << (31 - __builtin_clz(nr - 1u)) : 0u; sh; sh >>= 1)
+            if (j + sh < nr && (run_b[j + sh] & 0xffffu) <= r) j += sh;
+        const uint32_t ra = run_a[j], rb = run_b[j], len = ra >> 16;
+        lc_event(A, st0 + r, b * 32768u + (ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len), len, (rb >> 16) & 0xffu,
+                 rb >> 24);
+    }
+}
+// the placement by the predicted counts: tile k (kLSTile blocks) by workgroup k
+__device__ __forceinline__ void ld_place_tile(const LCArgs &A, uint32_t *buf, uint32_t *wsum, unsigned long long *s_pre) {
+    ls_tile(A, blockIdx.x, A.tstat0, A.start0, buf, wsum, s_pre, A.ready0);
+}
+
 constexpr uint32_t kLDLongDw = 128;
 static_assert(kLDLongDw * 4u * kLCSlots >= 32768u, "a block holds fewer long records than slots");
-__global__ __launch_bounds__(kLDThreads) void lc_dense_kernel(LCArgs A) {
-    __shared__ uint32_t dat[8192 + 4];  // the block (+ zero pad: header reads near its end)
-    __shared__ uint32_t nt[2 * kLDTabDwords];  // tables of z^4, z^8 (ld_map)
-    __shared__ uint32_t t0[256];
-    __shared__ uint32_t run_a[kLDRuns];  // offset in block | length << 16
-    __shared__ uint32_t run_b[kLDRuns];  // first event (of the pass) | type << 16 | kind << 24
-    __shared__ uint32_t s_m[3];          // per trip (mod 3): first failing candidate
-    __shared__ uint32_t s_bad;           // header offset of the block's first failing record
-    __shared__ unsigned long long s_seg;  // stash offset of the pass's segment (~0: did not fit)
-    __shared__ uint32_t s_c[3];           // the first three chunks, then [2]: the chunk after the next
-    __shared__ uint32_t doff[kDWMax / 2];  // lc_dwalk's header offsets of the block (u16 pairs)
-    __shared__ uint32_t s_inc;            // lc_dwalk's offsets disagree with the staged bytes
-    const uint32_t nd = uni(A.dense_ctr[0]);
-    uint32_t *const ctr = &A.dense_ctr[1];  // list entries taken
-    if (nd == 0) return;  // no dense block in the log
-    const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-    if (t == 0)
-        for (int k = 0; k < 3; k++) s_c[k] = atomicAdd(ctr, ld_chunk(nd));
-    t0[t] = A.aux[t];
-    if (t < 3) s_m[t] = kLCNone;
-    ld_sync();
-    for (uint32_t w = t; w < 2u * kLDTabDwords; w += kLDThreads) {
-        // F_k,i[v] = z^(4k)(v << 5i) at 224 (k-1) + 32 i + v (i = 6: v < 4, the rest unused)
-        const uint32_t k = w / kLDTabDwords + 1u, e = w % kLDTabDwords;
-        const uint32_t i = e >> 5, v = e & 31u;
-        uint32_t s = i * 5u < 32u ? v << (5u * i) : 0u;
-        for (uint32_t z = 0; z < 4u * k; z++) s = ld_z1(t0, s);
-        nt[w] = s;
-    }
-    ld_sync();
-    {  // t0 becomes the inverse table (ld_zi1): the stored crc is shifted back instead
-        const uint32_t e = t0[t];
-        ld_sync();
-        t0[e >> 24] = (e << 8) | t;
-    }
-    ld_sync();
-    const uint32_t *N4 = nt, *N8 = nt + kLDTabDwords;
-    // the first dword of a record whose crc range starts q & 3 = h bytes into a
-    // dword: W0 (value()'s seed, fed as the 4 bytes before the range) straddles
-    // it and the dword before, which holds W0 << 8h after zeros: C[h] = z^4(W0 << 8h)
-    const uint32_t W0 = A.seed0;
-    const uint32_t C1 = ld_map(N4, W0 << 8), C2 = ld_map(N4, W0 << 16), C3 = ld_map(N4, W0 << 24);
-    const LDTabs T{N4, N8, t0, W0, C1, C2, C3};
-    LDSched sch;
-    sch.nd = nd;
-    sch.ch = ld_chunk(nd);
-    sch.init(A, s_c[0], s_c[1]);
-    bool moved = false, grab = false;  // grab (thread 0): a chunk is being taken for s_c[2]
-    uint32_t grabbed = 0;
-    // list entries: block | kDWUniform when lc_walk left the block to this walk alone
-    uint64_t be = sch.next(A, s_c[2], &moved), b = be & ~(uint64_t)kDWUniform;
-    uint64_t bp = ~0ull;  // the previous block (its first_bad is written once its crc phase is done)
-    LDPre pre;
-    if (ld_vec(A, b)) pre.load(A.log + b * 32768u, t);
-    // lc_dwalk's offsets and info word of the block, fetched with its bytes
-    uint32_t pofs = 0, pinfo = 0;
-    if (b < A.n_blocks && !(be & kDWUniform)) {
-        pofs = ((const uint32_t *)(A.dw_off + b * kDWMax))[t];
-        pinfo = A.dw_info[b];
-    }
-    unsigned long long pool_lo = 0, pool_hi = 0;  // uniform: this workgroup's unused stash entries
-    uint32_t trip = 0;                            // walk trips (s_m slot = trip mod 3), uniform
-    while (b < A.n_blocks) {
-        const uint64_t bs = b * 32768u;
-        const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
-        const bool eof = blen < 32768u;
-        __builtin_amdgcn_s_setprio(2);
-        ld_sync();  // the previous block's readers of dat / runs / s_* are done
-        if (ld_vec(A, b)) {
-            pre.store(dat, t);
-        } else {  // the file's short last block (or an unaligned log): bytes, nothing past its end
-            const uint8_t *src = A.log + bs;
-            for (uint32_t o = t; o < 8192u; o += kLDThreads) {
-                uint32_t v = 0;
-                for (uint32_t j = 0; j < 4; j++)
-                    if (4u * o + j < blen) v |= (uint32_t)src[4u * o + j] << (8 * j);
-                dat[o] = v;
-            }
-        }
-        if (t < 4) dat[8192 + t] = 0;
-        doff[t] = pofs;
-        if (t <= 32u) run_b[t] = 0;  // the sort's bucket counts (lc_dwalk's pass)
-        const uint32_t dinfo = uni(pinfo);  // lc_dwalk: offsets | resume << 16 (0: none)
-        if (t == 0) {
-            // the previous block's failure, read after the barrier above: its crc
-            // phase ends with no barrier when it was the block's last pass, so a
-            // wave still checking records could atomicMin s_bad after thread 0
-            // had read it at that block's end (r4: a flip in the 178th record of
-            // a 194-record run went unreported, test_dense_list_in_chunks_random_lengths)
-            if (bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
-            s_bad = kLCNone;
-            s_inc = 0;
-        }
-        bp = b;
-        ld_sync();
-        const uint64_t bne = sch.next(A, s_c[2], &moved), bn = bne & ~(uint64_t)kDWUniform;  // loads during this block
-        if (moved && t == 0) {  // s_c[2] became the next chunk: take the one after (written below)
-            grabbed = atomicAdd(ctr, sch.ch);
-            grab = true;
-        }
-        if (ld_vec(A, bn)) pre.load(A.log + bn * 32768u, t);
-        pofs = pinfo = 0;
-        if (bn < A.n_blocks && !(bne & kDWUniform)) {
-            pofs = ((const uint32_t *)(A.dw_off + bn * kDWMax))[t];
-            pinfo = A.dw_info[bn];
-        }
-        __builtin_amdgcn_s_setprio(2);  // the walk's dependent LDS trips before other workgroups' crc lookups
-        uint32_t p = 0, total = 0;  // uniform: walk position, events of the finished passes
-        uint32_t dn = dinfo & 0xffffu;  // lc_dwalk's offsets (one OK record each; 0 once found inconsistent)
-        uint32_t dc = 0;                 // uniform: offsets taken
-        uint64_t seg0 = ~0ull;      // uniform: the block's first segment (stash offset | entries << 48)
-        uint64_t link = ~0ull;      // uniform: the previous segment's link slot
-        bool fit = true, done = false;
-        // one OK record's crc (header at h, payload length len) against its stored crc
-        auto check = [&](uint32_t h, uint32_t len) {
-            const uint32_t q = h + 6u, e = h + 7u + len;  // crc range: type || payload
-            const uint32_t nd = ((e + 3u) >> 2) - (q >> 2);
-            if (nd > kLDLongDw) {  // a long record: through the rounds instead (below)
-                // < kLCSlots for records of one chain (>= 513 B each); more would mean
-                // records that overlap: reported (cap_flag), never a write past the slots
-                const uint32_t k = atomicAdd(&A.nlong[b], 1u);
-                if (k >= kLCSlots) {
-                    atomicOr(A.cap_flag, kLCFlagInconsistent);
-                    return;
-                }
-                A.slots[b * kLCSlots + k] = (uint64_t)h | ((uint64_t)len << 16) | ((uint64_t)lds32u(dat, h) << 32);
-                lc_hist_global(A, b / kLCGroup, lc_geom((uint64_t)(uintptr_t)A.log + bs + q, 1u + len));
-                return;
-            }
-            if (!ld_crc_ok(dat, T, h, len)) atomicMin(&s_bad, h);
-        };
-        auto doff16 = [&](uint32_t r) { return (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu; };
-        while (!done) {
-            // the block's failure so far: read before this pass's crc atomics can change it
-            const bool crc = A.checksum && s_bad == kLCNone;
-            uint32_t nr = 0, nev = 0;
-            const bool dpass = dc < dn;  // uniform
-            if (dpass) {
-                // ---- lc_dwalk's records (<= kDWMax, one run each) in ONE crc phase,
-                // sorted by their step count G (descending, a counting sort in
-                // run_b / run_a): each wave's 64 records then take about the same
-                // number of steps.  Random lengths in 256-record passes ran every wave
-                // to the longest of its 64 records, and a 2nd pass for the last ~50
-                // on one wave (r5d: lc_dense 1.98 ms per 4 GiB against 1.08 for
-                // DBBench's blocks).  Bucket 32 - G (G <= 32; long records, deferred
-                // to the rounds: bucket 32, last).
-                const uint32_t m = dn;
-                const uint32_t resume = dinfo >> 16;
-                // lc_dwalk's offsets are trusted only as the chain the staged bytes
-                // give: offset 0 first, every record OK (rem >= 7 + len, not type 0 of
-                // length 0) and followed by the next offset (the last by the resume
-                // position).  Offsets that disagree (r5: a study build read different
-                // bytes in the two kernels; lc_dense then checked garbage ranges and
-                // wrote long-record slots past the block's, an aperture violation in
-                // crc_gv4) leave the block to this kernel's own walk from its start.
-                bool bad = m > kDWMax;
-                uint32_t bk[2] = {0u, 0u}, rk[2] = {0u, 0u};
-#pragma unroll
-                for (uint32_t i = 0; i < 2; i++) {
-                    const uint32_t r = t + 256u * i;
-                    if (!bad && r < m) {
-                        const uint32_t h = doff16(r), nx = r + 1u < m ? doff16(r + 1u) : resume;
-                        bad = (r == 0u && h != 0u) || blen < 7u || h > blen - 7u || nx > blen;
-                        const uint32_t key = bad ? 0u : lds32u(dat, h + 3u) >> 8, len = key & 0xffffu;
-                        bad = bad || key == 0u || h + 7u + len != nx;
-                        if (crc && !bad) {
-                            const uint32_t dw = ((h + 10u + len) >> 2) - ((h + 6u) >> 2);  // nd of check()
-                            bk[i] = dw > kLDLongDw ? 32u : 32u - ((dw + 3u) >> 2);
-                            rk[i] = atomicAdd(&run_b[bk[i]], 1u);
-                        }
-                    }
-                }
-                if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) atomicOr(&s_inc, 1u);
-                ld_sync();
-                if (uni(s_inc)) {  // the whole block through the walk passes below (run_b is theirs again)
-                    dn = dc = 0;
-                    p = 0;
-                    continue;
-                }
-                dc = dn;
-                p = resume;  // the block's rest: the walk below, from where lc_dwalk stopped
-                if (crc) {
-                    if (t < 64u) {  // bucket starts, after the 33 counts
-                        const uint32_t v = t <= 32u ? run_b[t] : 0u;
-                        const uint32_t ex = lc_wave_excl_sum(v);
-                        if (t <= 32u) run_b[64u + t] = ex;
-                    }
-                    ld_sync();
-                    uint16_t *perm = (uint16_t *)run_a;  // sorted position -> record
-#pragma unroll
-                    for (uint32_t i = 0; i < 2; i++)
-                        if (t + 256u * i < m) perm[run_b[64u + bk[i]] + rk[i]] = (uint16_t)(t + 256u * i);
-                    ld_sync();
-                    __builtin_amdgcn_s_setprio(0);
-                    for (uint32_t k = t; k < m; k += kLDThreads) {
-                        const uint32_t h = doff16(perm[k]);
-                        check(h, (lds32u(dat, h + 3u) >> 8) & 0xffffu);
-                    }
-                }
-                nr = nev = m;
-                // the walk from p ends at once, with no event (the block's trailer): no pass
-                done = blen - p < 7u && !(eof && blen - p > 0u);
-            } else {
-                // ---- walk: up to kLDRuns runs from p
-                uint32_t pk = ~0u;  // uniform: the last run's key (below) when its records are OK
-                while (nr < kLDRuns) {
-                    // header bytes 3..6 at p (p <= blen: the zero pad covers the block's
-                    // end); key = w >> 8 = length | type << 16
-                    const uint32_t rem = blen - p, w = uni(lds32u(dat, p + 3u)), key = w >> 8, len = key & 0xffffu;
-                    if (rem >= 7u + len && key != 0u) {  // lc_decide's kind 1: an OK record
-                        if (key == pk) {
-                            // it repeats the record before it: the run is measured from here
-                            // (thread t: the candidate p + (t + 1) L) and joins that record's;
-                            // one header read per record, no peek at the next (r4: records of
-                            // random lengths 6.9 -> 3.4 ms per GiB, tools/cliff_probe.py)
-                            const uint32_t L = 7u + len, c = p + (t + 1u) * L;
-                            const bool ok = c + L <= blen && (lds32u(dat, c + 3u) >> 8) == key;
-                            const uint64_t nok = __builtin_amdgcn_ballot_w64(!ok);
-                            const uint32_t slot = trip % 3u;
-                            if (lane == 0 && nok) atomicMin(&s_m[slot], 64u * wv + (uint32_t)__builtin_ctzll(nok));
-                            if (t == 0) s_m[(trip + 1u) % 3u] = kLCNone;  // its last readers passed the previous barrier
-                            ld_sync();
-                            const uint32_t f = uni(s_m[slot]);
-                            const uint32_t m = 1u + (f < kLDThreads ? f : kLDThreads);
-                            trip++;
-                            nev += m;
-                            p += m * L;
-                            continue;
-                        }
-                        // a new run (a block's leading fragment, a length change)
-                        if (t == 0) {
-                            run_a[nr] = p | (len << 16);
-                            run_b[nr] = nev | (w & 0xff000000u) >> 8 | (1u << 24);
-                        }
-                        nr++;
-                        pk = key;
-                        nev++;
-                        p += 7u + len;
-                        continue;
-                    }
-                    // the block's end: the trailer (no event) or a record that stops the walk
-                    const LCDecision d0 = lc_decide(rem, eof, rem >= 7u ? w : 0u);
-                    if (d0.kind != 0u) {
-                        if (t == 0) {
-                            run_a[nr] = p | (d0.length << 16);
-                            run_b[nr] = nev | (d0.type << 16) | (d0.kind << 24);
-                        }
-                        nr++;
-                        nev++;
-                    }
-                    done = true;
-                    break;
-                }
-                ld_sync();  // the pass's runs are in LDS
-                __builtin_amdgcn_s_setprio(0);
-                // ---- crc: one thread per OK record (none once the block has a failure:
-                // the records after it are dropped whatever their crc)
-                if (crc) {
-                    for (uint32_t r = t; r < nev; r += kLDThreads) {
-                        uint32_t j = 0;  // the run holding event r: the last with first <= r
-                        // steps from the largest power of two below nr (DBBench's blocks: 2-3 runs)
-                        for (uint32_t s = nr > 1u ? 1u << (31 - __builtin_clz(nr - 1u)) : 0u; s; s >>= 1)
-                            if (j + s < nr && (run_b[j + s] & 0xffffu) <= r) j += s;
-                        const uint32_t ra = run_a[j], rb = run_b[j];
-                        if ((rb >> 24) != 1u) continue;
-                        const uint32_t len = ra >> 16;
-                        check((ra & 0xffffu) + (r - (rb & 0xffffu)) * (7u + len), len);
-                    }
-                }
-            }
-            // ---- stash the pass's runs: one segment (+ a link slot when a pass follows).
-            // The stash state is uniform (every thread tracks it); thread 0's atomic
-            // reaches the others through LDS only when a pool is refilled (every ~69
-            // DBBench blocks) or, without pools (small logs), for every pass: no
-            // barrier in this phase otherwise (r4)
-            if (t == 0 && grab) {  // read by the next block's sch.next (after its barriers)
-                s_c[2] = grabbed;
-                grab = false;
-            }
-            const uint64_t n = nr + (done ? 0u : 1u);
-            unsigned long long so = ~0ull;
-            if (fit) {
-                if (!A.stash_pool) {
-                    if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)n);
-                    ld_sync();
-                    so = s_seg;
-                } else {  // a pass needs at most kDWMax + 1 <= kLDPool entries
-                    if (pool_hi - pool_lo < n) {
-                        if (t == 0) s_seg = atomicAdd(A.stash_ctr, (unsigned long long)A.stash_pool);
-                        ld_sync();
-                        pool_lo = s_seg;
-                        pool_hi = pool_lo + A.stash_pool;
-                    }
-                    so = pool_lo;
-                    pool_lo += n;
-                }
-                if (so + n > A.stash_cap) {  // past the stash: the caller's event array is too small
-                    fit = false;
-                    so = ~0ull;
-                } else if (link != ~0ull) {
-                    if (t == 0) A.stash[link] = (kLDLink << 56) | (n << 40) | so;
-                } else {
-                    seg0 = so | (n << 48);
-                }
-            }
-            link = done || !fit ? ~0ull : so + nr;
-            if (so != ~0ull) {
-                if (dpass) {  // record r: a run of one at its header, event r of the pass
-                    for (uint32_t r = t; r < nr; r += kLDThreads) {
-                        const uint32_t h = doff16(r), w = lds32u(dat, h + 3u);
-                        A.stash[so + r] = ld_run_entry(h | (w & 0xffff00u) << 8, r | (w & 0xff000000u) >> 8 | (1u << 24), 1u);
-                    }
-                } else if (t < nr) {
-                    const uint32_t first = run_b[t] & 0xffffu;
-                    const uint32_t next = t + 1u < nr ? run_b[t + 1u] & 0xffffu : nev;
-                    A.stash[so + t] = ld_run_entry(run_a[t], run_b[t], next - first);
-                }
-            }
-            total += nev;
-            if (!done) {
-                __builtin_amdgcn_s_setprio(2);
-                ld_sync();  // the next pass's walk rewrites the runs
-            }
-        }
-        if (t == 0) {
-            A.count[b] = total;
-            A.dense_off[b] = fit ? seg0 : ~0ull;
-        }
-        b = bn;
-    }
-    ld_sync();  // the last block's crc phase is done
-    if (t == 0 && bp != ~0ull && s_bad != kLCNone) A.first_bad[bp] = s_bad;
-}
+// Two kernels from one body (lc_dense_body.inc), either of them right for any log:
+// lc_dense_kernel (no in-place events: lc_build places every dense block) and
+// lc_dense_inplace_kernel (lc_dwalk's blocks' events in place when the log has
+// such blocks).  The host launches the second when the previous verification of
+// the workspace had lc_dwalk's blocks (LCArgs::hint, a guess that only decides
+// speed).  One kernel with both paths cost the DBBench set's lc_dense ~2.5 % (108
+// VGPRs and 75 SGPR spills against 101 and 45, r6w), out-of-line calls more
+// (scratch), a template kernel's instances took 132 VGPRs (3 workgroups per CU)
+// even with no change to the body, and both kernels launched (each returning at
+// once on the other's logs) cost every set an empty launch, ~4.6 us
+#define LD_KERNEL lc_dense_kernel
+#define LD_INPLACE 0
+#include "lc_dense_body.inc"
+#undef LD_KERNEL
+#undef LD_INPLACE
+#define LD_KERNEL lc_dense_inplace_kernel
+#define LD_INPLACE 1
+#include "lc_dense_body.inc"
+#undef LD_KERNEL
+#undef LD_INPLACE
 
 
 // ---------------------------------------------------------------------------
@@ -1696,8 +1501,11 @@ hipError_t launch_lc_dwalk(const LCArgs &A, hipStream_t st) {
     hipLaunchKernelGGL(lc_dwalk_kernel, dim3((A.n_blocks + 255u) / 256u), dim3(256), 0, st, A);
     return hipGetLastError();
 }
-hipError_t launch_lc_dense(const LCArgs &A, int cus, hipStream_t st) {
-    hipLaunchKernelGGL(lc_dense_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);
+hipError_t launch_lc_dense(const LCArgs &A, int cus, bool inplace, hipStream_t st) {
+    if (inplace)
+        hipLaunchKernelGGL(lc_dense_inplace_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);
+    else
+        hipLaunchKernelGGL(lc_dense_kernel, dim3(lc_dense_grid(cus)), dim3(kLDThreads), 0, st, A);
     return hipGetLastError();
 }
 

@@ -149,3 +149,63 @@ def test_inconsistent_dwalk_offsets_recovered(gpu, jl, oracle, maxlen):
         jl.set_option(jl.OPT_FAILPOINT, prev)
     assert int((w["kind"] == jl.LOG_BAD_CRC).sum()) >= 1
     _check(jl, oracle, log)  # and the same log without the failpoint
+
+
+def _segments(rng, shape):
+    """User record lengths for the in-place placement tests (each ~24 MiB of log):
+    random 0-200 B lengths (lc_dwalk's blocks), 131-B runs (lc_walk's run blocks),
+    both in alternating 2 MiB segments, and runs in which some pairs of records are
+    merged into one of the same bytes (2 x 131 + 7): blocks that pass the run checks
+    (lc_walk's equal records, lc_dwalk's two headers) but hold one event less than
+    predicted, among random blocks (the placement then falls back to lc_build)."""
+    def rand(nbytes):
+        return rng.integers(0, 201, nbytes // 107).astype(np.uint32)
+
+    def runs(nbytes, merge_every=0):
+        n = nbytes // 138
+        out = np.full(n, 131, np.uint32)
+        if merge_every:
+            keep = np.ones(n, bool)
+            for i in range(40, n - 1, merge_every):
+                out[i] = 2 * 131 + 7
+                keep[i + 1] = False
+            out = out[keep]
+        return out
+
+    seg = 2 << 20
+    if shape == "random":
+        return rand(24 << 20)
+    if shape == "runs":
+        return runs(24 << 20)
+    if shape == "mixed":
+        return np.concatenate([rand(seg) if k % 2 == 0 else runs(seg) for k in range(12)])
+    if shape == "mispredicted":
+        return np.concatenate([rand(seg) if k % 2 == 0 else runs(seg, 997 if k == 5 else 0) for k in range(12)])
+    raise ValueError(shape)
+
+
+@pytest.mark.parametrize("shape", ["random", "runs", "mixed", "mispredicted"])
+def test_inplace_events(gpu, jl, oracle, engine_options, shape):
+    """lc_dense writes the events of lc_dwalk's blocks in place, at starts placed by
+    the predicted event counts (lc_walk for run blocks, lc_dwalk for the others),
+    and lc_build keeps them only where the final count and start agree
+    (lc_dense_inplace_kernel, chosen when the workspace's last verification had
+    lc_dwalk's blocks).  Each log is verified three times in a row (the first
+    call after another log may take either kernel), flips included, and every
+    event must equal the oracle's (the device also lists the records a failure
+    drops, as kind 0: the live events are compared, as everywhere)."""
+    engine_options(jl.OPT_LOG_SMALL_MAX, 0)  # the chunked path at every size
+    rng = np.random.default_rng(SEED + len(shape))
+    log = _log(jl, gpu, _segments(rng, shape))
+    host = log.cpu().numpy().copy()
+    for b in rng.choice(host.size // 32768, 24, replace=False):  # a flip in 24 blocks
+        host[int(b) * 32768 + int(rng.integers(0, 32768))] ^= 0x10
+    import torch
+
+    log = torch.from_numpy(host).to(gpu)
+    want = oracle.log_events(host)
+    for _ in range(3):
+        ev, n = jl.log_verify_dev(log)
+        got = ev[: n * 16].cpu().numpy().view(jl.LOG_EVENT_DTYPE)
+        g, w = _live(got), _live(want)
+        assert g.shape == w.shape and np.array_equal(g, w)

@@ -20,7 +20,7 @@ def short(name):
         return "scans"
     if "crc_gv4_kernel<5" in name:
         return "crc_gv4_kernel<LOG_CHUNK>"
-    for k in ("lc_walk", "lc_dwalk", "lc_dense", "lc_build", "lc_setup", "lc_combine", "lc_apply"):
+    for k in ("lc_walk", "lc_dwalk", "lc_dense", "lc_dense_inplace", "lc_build", "lc_setup", "lc_combine", "lc_apply"):
         if k + "_kernel" in name:
             return k
     return None
