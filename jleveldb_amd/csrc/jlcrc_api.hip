@@ -1485,7 +1485,7 @@ static int log_verify_chunks(Workspace &c, const void *d_log, uint64_t log_bytes
     // walk (initialises count[nb], the hist tail, first_bad, cap_flag, the stash counter);
     // dense blocks: verified whole, exact counts, events stashed
     // [0] lc_walk's dense list, [1] lc_dense's chunk counter, [2] gv4 round batches, [3] lc_scan's work ids,
-    // [6] lc_dwalk's blocks
+    // [6] lc_dwalk's blocks, [7] those whose events it did not predict
     // (lc_finish zeroes them again at the end; r5 dropped the memset here: a
     // 4.4 us fill dispatch plus a ~6 us gap before it in every verification)
     if (c.lc_dirty) JL_HIP(hipMemsetAsync(A.dense_ctr, 0, 32, st));

@@ -636,7 +636,7 @@ __device__ __forceinline__ void lc_finish(const LCArgs &A) {
         A.result[2] = *A.cap_flag;
         lc_st16(A.dense_ctr, lc_v4{0u, 0u, 0u, 0u});
         if (A.hint) *A.hint = *A.nu_ctr;  // the host's guess for the next verification's lc_dense
-        lc_st16(A.dense_ctr + 4, lc_v4{0u, 0u, 0u, 0u});  // [6] nu_ctr
+        lc_st16(A.dense_ctr + 4, lc_v4{0u, 0u, 0u, 0u});  // [6] nu_ctr, [7] lc_dwalk's blocks not predicted
     }
 }
 
@@ -669,8 +669,12 @@ __global__ __launch_bounds__(64 * kLCBuildWaves) void lc_build_kernel(LCArgs A) 
 #pragma unroll
     for (uint32_t i = 0; i < kPer; i++) {
         const uint64_t b = (uint64_t)blockIdx.x * kLCGroup + wv + i * kLCBuildWaves;
-        if (doff[i] != kLCNotDense && doff[i] != ~0ull && (doff[i] & kLDPlaced))
-            doff[i] = cnt[i] == A.pred[b] && st[i] == A.start0[b] ? ~0ull : doff[i] & ~kLDPlaced;
+        if (doff[i] != kLCNotDense && doff[i] != ~0ull && (doff[i] & kLDPlaced)) {
+            const bool keep = cnt[i] == A.pred[b] && st[i] == A.start0[b];
+            // a block without stashed runs (lc_dense: every count predicted) cannot move
+            if (!keep && (doff[i] >> 48) == 0u && lane == 0) atomicOr(A.cap_flag, kLCFlagInconsistent);
+            doff[i] = keep ? ~0ull : doff[i] & ~kLDPlaced;
+        }
     }
     // a block's walk slots, or a dense block's first 64 stash entries (its runs)
 #pragma unroll
@@ -878,6 +882,7 @@ __device__ __forceinline__ void dw_block(const LCArgs &A, uint32_t i) {
         if (rem < 7u + (key & 0xffffu) || key == 0u) pred = n + 1u;
     }
     A.count[b] = A.pred[b] = pred;
+    if (pred == kLCDense) atomicAdd(&A.dense_ctr[7], 1u);  // lc_dense then stashes every block's runs
 }
 
 // lc_dwalk: one lane per listed dense block (dw_block)
