@@ -231,8 +231,8 @@ int get_ws(Workspace **out) {
 // staged pageable input at a third of our sessions' rate (BENCH_r05: a 16 MiB
 // table 1 140 vs 505 us on the device, the same 1 180 vs 1 150 us on the host),
 // so no fixed size is right everywhere.  The default (JL_HOST_THRESHOLD_AUTO)
-// measures instead: per entry point and size class the first calls alternate the
-// paths (three each, their median), then every call takes the faster one and the
+// measures instead: per entry point and size class the first calls run on each
+// path (three each, their median), then every call takes the faster one and the
 // other is re-measured every 16 / 64 / 256 calls (Dispatch below).  A threshold
 // >= 0 fixes the split.
 constexpr int64_t kHostThresholdDefault = JL_HOST_THRESHOLD_AUTO, kLogHostThresholdDefault = JL_HOST_THRESHOLD_AUTO;
@@ -263,8 +263,8 @@ Options &opt() {
 
 // ------------------------------------------------------------ call dispatch
 // Auto dispatch state: per kind of call (the entry point) and size class (2^17 ..
-// 2^25 bytes), the two paths' cost per byte.  A class first alternates the paths
-// until each has kDispProbe calls (the median of those: a cold first call, page
+// 2^25 bytes), the two paths' cost per byte.  A class first runs kDispProbe calls
+// on the device, then kDispProbe on the host (the median of each: a cold first call, page
 // faults of a fresh buffer, do not decide it), then every call takes the cheaper
 // path and feeds its average; the other path is measured again every 16 calls
 // when the two are within 25 %, every 64 within 2x, else every 256 (a box whose
@@ -311,7 +311,11 @@ struct Route {
             std::lock_guard<std::mutex> lk(D.mu);
             Dispatch::Cell &c = D.cell[kind][bucket];
             if (c.n[0] < kDispProbe || c.n[1] < kDispProbe) {
-                host = c.n[0] < c.n[1];  // alternate, the device first
+                // the device's probes first, then the host's: alternated, a device call
+                // after a host call (whose start ends the copy pool's spinning) paid
+                // the workers' wake-up, and the probes chose the host for a 4 MiB table
+                // that the device verifies in 204 against 287 us (r6zb)
+                host = c.n[1] >= kDispProbe;
             } else {
                 const bool h = c.ns_per_byte[0] <= c.ns_per_byte[1];
                 const double r = h ? c.ns_per_byte[1] / c.ns_per_byte[0] : c.ns_per_byte[0] / c.ns_per_byte[1];

@@ -89,8 +89,8 @@ def test_threshold_option(jl, gpu, engine_options):
 
 @pytest.mark.parametrize("kind", ["table", "log"])
 def test_auto_dispatch(gpu, jl, oracle, engine_options, kind):
-    """JL_HOST_THRESHOLD_AUTO: in a size class the first calls alternate the paths
-    until each ran three times (JL_INFO_LAST_PATH shows which), every call's
+    """JL_HOST_THRESHOLD_AUTO: in a size class the first calls run three times on
+    the device, then three times on the host (JL_INFO_LAST_PATH shows which), every call's
     output is the same, and then the calls keep to one path, the other measured
     again every 16 / 64 / 256 calls."""
     rng = np.random.default_rng(SEED + 5)
@@ -113,7 +113,7 @@ def test_auto_dispatch(gpu, jl, oracle, engine_options, kind):
         paths.append(jl.get_option(jl.INFO_LAST_PATH))
         assert jl.get_option(jl.INFO_LAST_CALL_NS) > 0
     assert all(np.array_equal(o, outs[0]) for o in outs)
-    assert paths[:6] == [1, 0, 1, 0, 1, 0], paths  # alternating, the device first
+    assert paths[:6] == [1, 1, 1, 0, 0, 0], paths  # three on the device, then three on the host
     later = paths[6:]
     assert min(later.count(0), later.count(1)) <= 3, paths  # one path kept, the other re-measured
 
