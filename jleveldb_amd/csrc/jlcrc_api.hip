@@ -884,7 +884,7 @@ int jl_set_option(int option, int64_t value) {
         o.failpoint = (int)value;
         return JL_OK;
     case JL_OPT_LOG_SMALL_MAX:
-        if (value < 0 || value > (int64_t)1 << 40) break;  // host-memory logs: at most one chunk
+        if (value < 0 || value > (int64_t)JL_STREAM_CHUNK_BYTES) break;
         o.log_small_max = value;
         return JL_OK;
     default:
@@ -1741,7 +1741,7 @@ int jl_log_verify(const uint8_t *log, uint64_t log_bytes, int checksum, jl_log_e
     Workspace *w = nullptr;
     if (int r = get_ws(&w)) return r;
     if (int r = ws_order(*w, w->stream)) return r;
-    if (small_log(log_bytes, checksum) && log_bytes <= JL_STREAM_CHUNK_BYTES) {
+    if (small_log(log_bytes, checksum)) {
         const int rc = log_verify_small_host(*w, log, log_bytes, checksum != JL_LOG_NO_CHECKSUM, events, cap, n_events);
         if (rc) (void)hipStreamSynchronize(w->stream);  // nothing of the call left in flight
         w->async_pending = false;  // w->stream waited for any earlier asynchronous call, and it is done
