@@ -53,6 +53,7 @@ class CopyPool {
                 }
             }
             live_.store((int)th_.size());
+            th_count_.store((int)th_.size(), std::memory_order_relaxed);
             q_.push_back(&j);
             queued_.fetch_add(1);
         }
@@ -71,6 +72,18 @@ class CopyPool {
     // spinning: spinners share the caller's cores (SMT siblings) and slowed the
     // host path right after a device call, which misled the auto dispatch's probes
     void quiesce() { epoch_.fetch_add(1, std::memory_order_relaxed); }
+    // a caller about to stage for the device wakes the sleeping workers first: they
+    // spin (kSpinUs) while the call sets up, instead of taking the futex wake-up on
+    // the copy's path (a device call right after host calls staged 8 MiB at ~22 GB/s,
+    // one core's rate, r6zc)
+    void prewake() {
+        if (th_count_.load(std::memory_order_relaxed) == 0) return;  // no workers yet
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            wake_++;
+        }
+        cv_.notify_all();
+    }
     int workers() const { return live_.load(); }  // threads running
     int spawn_failures() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -105,6 +118,7 @@ class CopyPool {
     }
     void work() {
         std::unique_lock<std::mutex> lk(mu_);
+        uint64_t seen = wake_;  // prewake() calls seen (guarded by mu_)
         for (;;) {
             if (q_.empty() && !stop_) {  // spin a while (unlocked) before sleeping
                 lk.unlock();
@@ -115,8 +129,10 @@ class CopyPool {
                     __builtin_ia32_pause();
                 lk.lock();
             }
-            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            cv_.wait(lk, [&] { return stop_ || !q_.empty() || wake_ != seen; });
             if (stop_) return;
+            seen = wake_;
+            if (q_.empty()) continue;  // woken ahead of a copy: spin for it
             Job *j = q_.front();
             if (j->next.load() >= j->pieces) {  // every piece taken: the job leaves the queue
                 q_.pop_front();
@@ -136,6 +152,8 @@ class CopyPool {
     std::deque<Job *> q_;
     std::atomic<int> queued_{0};  // jobs in q_ (read by spinning workers without the lock)
     std::atomic<uint64_t> epoch_{0};  // quiesce() calls: a change ends the workers' spinning
+    uint64_t wake_ = 0;                 // prewake() calls (guarded by mu_)
+    std::atomic<int> th_count_{0};      // th_.size() for prewake's quick check
     std::vector<std::thread> th_;
     bool stop_ = false;
     int failures_ = 0;                                // threads that could not start (guarded by mu_)

@@ -326,6 +326,7 @@ struct Route {
         }
         t_last_path = host ? 0 : 1;
         if (host) copy_pool().quiesce();
+        else copy_pool().prewake();  // (the call's staging copies, if its input is pageable)
     }
     ~Route() {
         const int64_t ns =

@@ -30,6 +30,10 @@ int main(int argc, char **argv) {
             const size_t n = sizes[rnd() % 6] + rnd() % 4096;
             std::vector<uint8_t> src(n), dst(n, 0xee);
             for (size_t i = 0; i < n; i += 8) src[i] = (uint8_t)(rnd() >> 11);
+            // the dispatch's hints around the copies: a host-path call ends the
+            // workers' spinning, a device-path call wakes them ahead of its copy
+            if (rnd() % 3 == 0) pool.quiesce();
+            if (rnd() % 3 == 0) pool.prewake();
             pool.copy(dst.data(), src.data(), n, 1 + (int)(rnd() % 8));
             if (memcmp(dst.data(), src.data(), n) != 0) bad++;
         }
