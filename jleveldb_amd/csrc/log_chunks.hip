@@ -1150,9 +1150,17 @@ __device__ __forceinline__ uint64_t ld_run_entry(uint32_t ra, uint32_t rb, uint3
 // lc_dense's in-place events (lc_dwalk's blocks; only lc_dense_kernel<true>).
 // The block's first event's place (lc_dense's first workgroups' placement, once
 // its tile is out).
+// its tile out; bounded (~0.2 s): past that the call is reported inconsistent
+// and the block's events are not written, never a hang
 __device__ __forceinline__ uint64_t ld_start0(const LCArgs &A, uint64_t b) {
-    while (__hip_atomic_load(&A.ready0[b / kLSTile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.gen)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&A.ready0[b / kLSTile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.gen) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // (100 MHz clock)
+            if (threadIdx.x == 0) atomicOr(A.cap_flag, kLCFlagInconsistent);
+            return ~0ull >> 1;
+        }
         __builtin_amdgcn_s_sleep(2);
+    }
     return uni64(__hip_atomic_load(&A.start0[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 // events [ev0, ev0 + m) of block b: lc_dwalk's records, one each (header offsets doff)
@@ -1178,9 +1186,15 @@ __device__ __forceinline__ void ld_place_runs(const LCArgs &A, const uint32_t *r
                  rb >> 24);
     }
 }
-// the placement by the predicted counts: tile k (kLSTile blocks) by workgroup k
+// the placement by the predicted counts: tiles k, k + grid, ... (kLSTile blocks
+// each) by workgroup k (every workgroup does its first tile first, so a tile's
+// look-back only waits for tiles already under way)
 __device__ __forceinline__ void ld_place_tile(const LCArgs &A, uint32_t *buf, uint32_t *wsum, unsigned long long *s_pre) {
-    ls_tile(A, blockIdx.x, A.tstat0, A.start0, buf, wsum, s_pre, A.ready0);
+    const uint32_t tiles = (A.n_blocks + kLSTile) / kLSTile;
+    for (uint32_t k = blockIdx.x; k < tiles; k += gridDim.x) {
+        ls_tile(A, k, A.tstat0, A.start0, buf, wsum, s_pre, A.ready0);
+        __syncthreads();  // buf / wsum / s_pre reused
+    }
 }
 
 constexpr uint32_t kLDLongDw = 128;
