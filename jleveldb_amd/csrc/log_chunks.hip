@@ -812,26 +812,53 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2).
 // One listed dense block (lc_dwalk's lane): a run block's prediction checked, the
 // others' headers walked and their events predicted (count[b] = pred[b]).
+__device__ __forceinline__ uint32_t dw_blen(const LCArgs &A, uint64_t b) {
+    const uint64_t bs = b * 32768u;
+    return (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+}
+// A run block's (kDWUniform) prediction holds, or nothing needs it.  lc_walk: a
+// run, lc_dense walks it.  Its predicted event count (lc_walk's, from the walked
+// records) places the blocks after it, which matters only when lc_dense writes
+// events in place (some dense block is lc_dwalk's): checked at two headers, the
+// next one repeats the run's length and the one after the run's predicted end
+// fills the block.  A block of records of random lengths whose last walked ones
+// were equal by chance fails and is walked by lc_dwalk instead (a wrong
+// prediction costs lc_build the blocks after it)
+__device__ __forceinline__ bool dw_run_holds(const LCArgs &A, uint64_t b) {
+    if (*A.nu_ctr == 0u) return true;
+    const uint64_t bs = b * 32768u;
+    const uint32_t blen = dw_blen(A, b);
+    const uint32_t info = A.dw_info[b], p = info & 0xffffu, L = info >> 16, left = blen - p;
+    const uint32_t rem = left % L, k = left / L;
+    const uint64_t h1 = k ? lc_header(A.log + bs + p, left) : 0ull;
+    const uint64_t h2 = rem >= 7u ? lc_header(A.log + bs + p + k * L, rem) : 0ull;
+    const bool ok1 = !k || 7u + ((uint32_t)(h1 >> 32) & 0xffffu) == L;
+    const bool ok2 = rem < 7u || 7u + ((uint32_t)(h2 >> 32) & 0xffffu) == rem;
+    return ok1 && ok2;
+}
+// the block's predicted events (count[b] = pred[b]) once its walk stopped at p
+// after n offsets: the walk ended at the block's end (then the trailer, or the
+// file's short last block's kind-6 event) or at a record that is not OK (`bad`:
+// its event ends lc_dense's walk); after a run or kDWMax offsets: not predicted
+// (kLCDense: the placement of the blocks after it is lc_build's)
+__device__ __forceinline__ void dw_predict(const LCArgs &A, uint64_t b, uint32_t blen, uint32_t p, uint32_t n,
+                                           bool bad) {
+    A.dw_info[b] = n | (p << 16);
+    const uint32_t rem = blen - p;
+    uint32_t pred = kLCDense;
+    if (rem < 7u)
+        pred = n + (blen < 32768u && rem > 0u ? 1u : 0u);
+    else if (bad)
+        pred = n + 1u;
+    A.count[b] = A.pred[b] = pred;
+    if (pred == kLCDense) atomicAdd(&A.dense_ctr[7], 1u);  // lc_dense then stashes every block's runs
+}
 __device__ __forceinline__ void dw_block(const LCArgs &A, uint32_t i) {
     const uint32_t e = A.dense_list[i];
     const uint64_t b = e & ~kDWUniform, bs = b * 32768u;
-    const uint32_t blen = (uint32_t)(A.size - bs < 32768u ? A.size - bs : 32768u);
+    const uint32_t blen = dw_blen(A, b);
     if (e & kDWUniform) {
-        // lc_walk: a run, lc_dense walks it.  Its predicted event count (lc_walk's,
-        // from the walked records) places the blocks after it, which matters only
-        // when lc_dense writes events in place (some dense block is lc_dwalk's):
-        // checked at two headers, the next one repeats the run's length and the one
-        // after the run's predicted end fills the block.  A block of records of
-        // random lengths whose last walked ones were equal by chance fails and is
-        // walked here instead (a wrong prediction costs lc_build the blocks after it)
-        if (*A.nu_ctr == 0u) return;
-        const uint32_t info = A.dw_info[b], p = info & 0xffffu, L = info >> 16, left = blen - p;
-        const uint32_t rem = left % L, k = left / L;
-        const uint64_t h1 = k ? lc_header(A.log + bs + p, left) : 0ull;
-        const uint64_t h2 = rem >= 7u ? lc_header(A.log + bs + p + k * L, rem) : 0ull;
-        const bool ok1 = !k || 7u + ((uint32_t)(h1 >> 32) & 0xffffu) == L;
-        const bool ok2 = rem < 7u || 7u + ((uint32_t)(h2 >> 32) & 0xffffu) == rem;
-        if (ok1 && ok2) return;
+        if (dw_run_holds(A, b)) return;
         A.dense_list[i] = (uint32_t)b;  // not a run after all: walked here, its offsets to lc_dense
     }
     const uint8_t *blk = A.log + bs;
@@ -868,21 +895,13 @@ __device__ __forceinline__ void dw_block(const LCArgs &A, uint32_t i) {
         }
         if (n > n0) out[n0 / 8u] = lc_v4{q[0], q[1], q[2], q[3]};
     }
-    A.dw_info[b] = n | (p << 16);
-    // the block's events when the walk ended at its end (then the trailer, or the
-    // file's short last block's kind-6 event) or at a record that is not OK (its
-    // event ends lc_dense's walk); after a run or kDWMax offsets: not predicted
-    // (kLCDense: the placement of the blocks after it is lc_build's)
     const uint32_t rem = blen - p;
-    uint32_t pred = kLCDense;
-    if (rem < 7u) {
-        pred = n + (blen < 32768u && rem > 0u ? 1u : 0u);
-    } else if (n < kDWMax) {
+    bool bad = false;
+    if (rem >= 7u && n < kDWMax) {
         const uint32_t key = (uint32_t)(lc_header(blk + p, rem) >> 32) & 0xffffffu;
-        if (rem < 7u + (key & 0xffffu) || key == 0u) pred = n + 1u;
+        bad = rem < 7u + (key & 0xffffu) || key == 0u;
     }
-    A.count[b] = A.pred[b] = pred;
-    if (pred == kLCDense) atomicAdd(&A.dense_ctr[7], 1u);  // lc_dense then stashes every block's runs
+    dw_predict(A, b, blen, p, n, bad);
 }
 
 // lc_dwalk: one lane per listed dense block (dw_block)
