@@ -809,7 +809,8 @@ __global__ __launch_bounds__(256) void lc_apply_kernel(LCArgs A) {
 // Offsets are u16 (p < 32 KiB), eight per 16-B store.  The walk reads nearly
 // every line of its blocks at the HBM's random-line rate: a line prefetch 256 or
 // 512 B ahead of each lane's walk made it slower (r5p, random 0-200 B set 2.62 ->
-// 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2).
+// 2.90 / 3.07 ms: the extra lines in flight evict the walk's own from L2), and so
+// did a load of the next line beside each hop (r6zh, 2.53 -> 2.91 ms).
 // One listed dense block (lc_dwalk's lane): a run block's prediction checked, the
 // others' headers walked and their events predicted (count[b] = pred[b]).
 __device__ __forceinline__ uint32_t dw_blen(const LCArgs &A, uint64_t b) {
