@@ -6,9 +6,6 @@
 
 #include "engine_device.hpp"
 
-#ifndef JL_STUDY
-#define JL_STUDY 0
-#endif
 #ifndef JL_MODE
 #error "compile with -DJL_MODE=<jlk::MODE_*>"
 #endif
