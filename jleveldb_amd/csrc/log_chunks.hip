@@ -1176,7 +1176,7 @@ __device__ __forceinline__ uint64_t ld_start0(const LCArgs &A, uint64_t b) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(&A.ready0[b / kLSTile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != A.gen) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // (100 MHz clock)
-            if (threadIdx.x == 0) atomicOr(A.cap_flag, kLCFlagInconsistent);
+            if ((threadIdx.x & 63u) == 0u) atomicOr(A.cap_flag, kLCFlagInconsistent);  // (any wave may wait)
             return ~0ull >> 1;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -1185,9 +1185,9 @@ __device__ __forceinline__ uint64_t ld_start0(const LCArgs &A, uint64_t b) {
 }
 // events [ev0, ev0 + m) of block b: lc_dwalk's records, one each (header offsets doff)
 __device__ __forceinline__ void ld_place_dw(const LCArgs &A, const uint32_t *dat, const uint32_t *doff, uint64_t b,
-                                         uint32_t ev0, uint32_t m) {
+                                         uint32_t ev0, uint32_t m, uint32_t r0, uint32_t stride) {
     const uint64_t st0 = ld_start0(A, b) + ev0;
-    for (uint32_t r = threadIdx.x; r < m; r += 256u) {
+    for (uint32_t r = r0; r < m; r += stride) {
         const uint32_t h = (doff[r >> 1] >> (16u * (r & 1u))) & 0xffffu;
         const uint32_t w = __builtin_amdgcn_alignbyte(dat[((h + 3u) >> 2) + 1u], dat[(h + 3u) >> 2], (h + 3u) & 3u);
         lc_event(A, st0 + r, b * 32768u + h, (w >> 8) & 0xffffu, w >> 24, 1u);
